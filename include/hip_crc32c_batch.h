@@ -1,0 +1,163 @@
+/*
+ * hip_crc32c_batch.h -- C-ABI of the MI355X batched CRC32C engine.
+ *
+ * The boundary between WipDB's C++ table layer and the HIP kernels.  Plain
+ * pointers and sizes only; no C++ or torch types cross it; nothing throws.
+ *
+ * What each entry point replaces in the reference (/root/reference):
+ *
+ *   hcrc_batch / hcrc_batch_async
+ *       N calls of kv::crc32c::Extend(init_crc, data, n)
+ *       (kv/src/util/crc32c.h:24, kv/src/util/crc32c.cc:1225-1227), as made
+ *       one block at a time by TableBuilder::WriteRawBlock
+ *       (kv/src/table/table_builder.cc:194-196) and ReadBlock
+ *       (kv/src/table/format.cc:91-93).  With HCRC_MASK_OUTPUT the stored
+ *       form kv::crc32c::Mask(crc) (kv/src/util/crc32c.h:38-41) is written.
+ *       leveldb::crc32c::Extend (leveldb/util/crc32c.h:17,
+ *       leveldb/util/crc32c.cc:275) is the same function.
+ *   hcrc_batch_strided_async
+ *       the same for fixed-size, fixed-stride blocks (no descriptor arrays).
+ *   hcrc_verify_async
+ *       ReadBlock's check (kv/src/table/format.cc:91-99):
+ *       Unmask(stored) == Value(data, n+1) for a batch of blocks.
+ *   hcrc_batch_multi
+ *       a batch sharded by bytes over several GPUs of one node (no
+ *       collective: blocks are independent).
+ *   hcrc_cpu_extend / hcrc_cpu_batch
+ *       the host CPU path (from scratch, SSE4.2+PCLMUL or portable), i.e.
+ *       what kv::crc32c::Extend itself does on the host.
+ *
+ * Semantics shared by every batch call (bit-exact with the reference):
+ *   out[i] = Extend(inits ? inits[i] : 0, base + offsets[i], lengths[i])
+ *   optionally Mask()-ed.  Any span alignment, any length >= 0 (a length
+ *   of 0 returns the init value, as Extend does).
+ *
+ * Ownership: the caller owns base/offsets/lengths/inits/out and keeps them
+ * valid until the call (sync) or the stream (async) completes.  The context
+ * owns device tables, staging buffers and its stream.  No pointer is
+ * retained after completion.
+ *
+ * Errors: 0 on success, a negative HCRC_ERR_* code otherwise.  The batch
+ * entry points never fall back to the CPU silently; a caller that wants a
+ * fallback (the C++ wrapper's AUTO policy) calls hcrc_cpu_batch itself.
+ *
+ * Threading: a context may be used from several threads; calls on one
+ * context are serialised by an internal mutex (async calls on
+ * caller-provided streams only hold it while enqueueing).
+ */
+#ifndef HIP_CRC32C_BATCH_H_
+#define HIP_CRC32C_BATCH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HCRC_ABI_VERSION 1
+
+/* return codes */
+#define HCRC_OK 0
+#define HCRC_ERR_INVALID (-1)   /* bad argument (null pointer, bad flags) */
+#define HCRC_ERR_NO_DEVICE (-2) /* no HIP device or bad device index     */
+#define HCRC_ERR_NO_MEMORY (-3) /* device or pinned allocation failed    */
+#define HCRC_ERR_HIP (-4)       /* other HIP runtime error               */
+#define HCRC_ERR_LAUNCH (-5)    /* kernel launch failed                  */
+#define HCRC_ERR_MISMATCH (-6)  /* hcrc_verify*: at least one bad block  */
+
+/* flags */
+#define HCRC_HOST_PTRS 0x0    /* all array/data pointers are host memory    */
+#define HCRC_DEVICE_PTRS 0x1  /* all array/data pointers are device memory  */
+#define HCRC_MASK_OUTPUT 0x2  /* write Mask(crc) instead of crc             */
+
+typedef struct hcrc_ctx hcrc_ctx;
+
+/* Library / device queries. */
+int hcrc_abi_version(void);
+int hcrc_device_count(int* count);
+const char* hcrc_strerror(int code);
+
+/* One context per device (idempotent per thread of use). */
+int hcrc_ctx_create(int device, hcrc_ctx** out_ctx);
+int hcrc_ctx_destroy(hcrc_ctx* ctx);
+/* The context's own HIP stream (hipStream_t as void*). */
+void* hcrc_ctx_stream(hcrc_ctx* ctx);
+int hcrc_ctx_device(hcrc_ctx* ctx);
+
+/* Synchronous batch.  HCRC_HOST_PTRS: data is staged through pinned
+ * buffers (H2D + kernel + D2H, overlapped); HCRC_DEVICE_PTRS: all pointers
+ * are device memory.  Returns after out[] is written. */
+int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets,
+               const uint32_t* lengths, const uint32_t* init_crcs,
+               uint32_t* out_crcs, size_t count, int flags);
+
+/* Asynchronous batch on device memory, enqueued on `stream` (a hipStream_t;
+ * NULL = the context's stream).  Requires HCRC_DEVICE_PTRS in flags. */
+int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base,
+                     const uint64_t* d_offsets, const uint32_t* d_lengths,
+                     const uint32_t* d_init_crcs, uint32_t* d_out_crcs,
+                     size_t count, int flags, void* stream);
+
+/* Fixed-size blocks: span i = d_base + i*stride, `length` bytes, all with
+ * the same init_crc.  Device memory, asynchronous on `stream`. */
+int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base,
+                             uint64_t stride, uint32_t length,
+                             uint32_t init_crc, uint32_t* d_out_crcs,
+                             size_t count, int flags, void* stream);
+
+/* Read-side verification (ReadBlock, kv/src/table/format.cc:91-99): block i
+ * is d_base + offsets[i] with handle size lengths[i] = n; the checksum
+ * covers n+1 bytes (contents + type byte) and is compared with the masked
+ * crc stored little-endian at byte n+1.  d_status[i] = 1 if it matches,
+ * 0 if not.  Asynchronous on `stream`, device memory. */
+int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base,
+                      const uint64_t* d_offsets, const uint32_t* d_lengths,
+                      uint8_t* d_status, size_t count, void* stream);
+
+/* Wait for all work on `stream` (NULL = the context's stream). */
+int hcrc_sync(hcrc_ctx* ctx, void* stream);
+
+/* Host-memory batch sharded over `ndev` devices by bytes, one host thread
+ * and context per device; results land in disjoint slices of out_crcs. */
+int hcrc_batch_multi(const int* devices, int ndev, const void* base,
+                     const uint64_t* offsets, const uint32_t* lengths,
+                     const uint32_t* init_crcs, uint32_t* out_crcs,
+                     size_t count, int flags);
+
+/* Pinned host memory (for zero-copy-free staging by the caller). */
+int hcrc_host_alloc(size_t bytes, void** out_ptr);
+int hcrc_host_free(void* ptr);
+
+/* Diagnostic: the measured read-stream ceiling.  Reads `count` fixed-size
+ * blocks like hcrc_batch_strided_async but only XOR-reduces them (same
+ * bytes in, 4 bytes out per block).  Used for the roofline denominator. */
+int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
+                          uint32_t length, uint32_t* d_out, size_t count,
+                          void* stream);
+
+/* Test/bench data: fills nbytes (multiple of 8, 8-byte aligned) of device
+ * memory with the seeded splitmix64 stream whose 64-bit word k is
+ * mix(seed + (first_word + k + 1) * 0x9E3779B97F4A7C15), so the host can
+ * regenerate any block for parity checks (tests/golden/common.py). */
+int hcrc_fill_splitmix64_async(hcrc_ctx* ctx, void* d_dst, uint64_t nbytes,
+                               uint64_t seed, uint64_t first_word,
+                               void* stream);
+
+/* Host CPU path (from-scratch SSE4.2+PCLMUL 3-stream, or portable
+ * slicing-by-8); the function kv::crc32c::Extend is built on. */
+uint32_t hcrc_cpu_extend(uint32_t init_crc, const void* data, size_t n);
+int hcrc_cpu_batch(const void* base, const uint64_t* offsets,
+                   const uint32_t* lengths, const uint32_t* init_crcs,
+                   uint32_t* out_crcs, size_t count, int flags, int threads);
+int hcrc_cpu_is_accelerated(void);
+
+/* Mask / Unmask of kv/src/util/crc32c.h:38-47. */
+uint32_t hcrc_mask(uint32_t crc);
+uint32_t hcrc_unmask(uint32_t masked_crc);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* HIP_CRC32C_BATCH_H_ */

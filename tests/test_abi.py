@@ -1,0 +1,71 @@
+"""The C-ABI boundary without a GPU: the library loads, exports every symbol
+include/hip_crc32c_batch.h declares, validates arguments, and the C++ drop-in
+surface (include/wipdb/crc32c.h) compiles and passes the reference's tests."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from wipdb_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # and every prototype the binding declares is in the header
+    assert set(_lib._PROTOS) == set(syms)
+
+
+def test_abi_version_and_strerror():
+    lib = _lib.load()
+    assert lib.hcrc_abi_version() == 1
+    for code in (0, -1, -2, -3, -4, -5, -6, -99):
+        assert lib.hcrc_strerror(code)
+
+
+def test_invalid_arguments_are_rejected_without_device():
+    lib = _lib.load()
+    assert lib.hcrc_ctx_create(0, None) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_ctx_destroy(None) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_batch(None, None, None, None, None, None, 0, 0) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_batch_async(None, None, None, None, None, None, 0, 1, None) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_sync(None, None) == _lib.HCRC_ERR_INVALID
+    devs = (ctypes.c_int * 1)(0)
+    assert lib.hcrc_batch_multi(devs, 0, None, None, None, None, None, 0, 0) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_cpu_batch(None, None, None, None, None, 1, 0, 1) == _lib.HCRC_ERR_INVALID
+    n = ctypes.c_int(-1)
+    rc = lib.hcrc_device_count(ctypes.byref(n))
+    assert (rc == 0 and n.value >= 0) or (rc == _lib.HCRC_ERR_NO_DEVICE and n.value == 0)
+
+
+def test_ctx_create_bad_device_index():
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    assert lib.hcrc_ctx_create(10_000, ctypes.byref(ctx)) == _lib.HCRC_ERR_NO_DEVICE
+    assert not ctx.value
+
+
+def _build_surface_test(tmp_path):
+    exe = str(tmp_path / "test_surface")
+    libdir = os.path.join(REPO, "wipdb_amd", "lib")
+    cmd = ["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
+           os.path.join(REPO, "tests", "cpp", "test_surface.cc"), "-L", libdir,
+           "-lhip_crc32c_batch", f"-Wl,-rpath,{libdir}", "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_cpp_surface_drop_in_cpu(tmp_path):
+    from tests.conftest import gpu_available
+    if gpu_available():
+        pytest.skip("GPU present: covered by tests/test_gpu_parity.py::test_cpp_surface_drop_in_gpu")
+    exe = _build_surface_test(tmp_path)
+    r = subprocess.run([exe, "0"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout

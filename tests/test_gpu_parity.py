@@ -1,0 +1,237 @@
+"""Parity of the HIP path with the oracle (and the compiled reference) on the
+GPU.  Every call goes through the C-ABI (wipdb_amd.Engine -> libhip_crc32c_batch).
+
+Bar: bit-exact (integer path).  Sizes the oracle finishes in seconds are
+compared CRC-for-CRC with the oracle; the full BASELINE size (1 M x 4 KiB,
+device-generated) is compared with the compiled reference (oracle/_ref,
+8 threads) plus an oracle sample, and with the size-independent stitching
+property Extend(Extend(c, A), B) == Extend(c, A||B).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _t(arr, dtype=None):
+    import torch
+    a = np.ascontiguousarray(arr)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).to("cuda:0")
+
+
+def _u32(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _run_device(engine, buf, offs, lens, inits=None, mask=False):
+    out = engine.batch_device(_t(buf), _t(np.asarray(offs, np.uint64)),
+                              _t(np.asarray(lens, np.uint32)),
+                              None if inits is None else _t(np.asarray(inits, np.uint32)),
+                              mask_output=mask)
+    return _u32(out)
+
+
+def test_golden_spans_device(engine, golden_spans):
+    g = golden_spans
+    got = _run_device(engine, g["buf"], g["offsets"], g["lengths"], g["inits"])
+    np.testing.assert_array_equal(got, g["crc"])
+    got = _run_device(engine, g["buf"], g["offsets"], g["lengths"], g["inits"], mask=True)
+    np.testing.assert_array_equal(got, g["masked"])
+
+
+def test_golden_spans_host_path(engine, golden_spans):
+    g = golden_spans
+    got = engine.batch(g["buf"], g["offsets"], g["lengths"], g["inits"])
+    np.testing.assert_array_equal(got, g["crc"])
+    got = engine.batch(g["buf"], g["offsets"], g["lengths"], g["inits"], mask_output=True)
+    np.testing.assert_array_equal(got, g["masked"])
+
+
+def test_kats_on_gpu(engine, oracle, kats):
+    rows = [bytes.fromhex(v["data_hex"]) for v in kats["rfc"]]
+    buf = np.frombuffer(b"".join(rows), dtype=np.uint8).copy()
+    offs = np.cumsum([0] + [len(r) for r in rows[:-1]]).astype(np.uint64)
+    lens = np.array([len(r) for r in rows], np.uint32)
+    got = _run_device(engine, buf, offs, lens)
+    assert [int(x) for x in got] == [v["crc"] for v in kats["rfc"]]
+    f = kats["folly"]
+    fb = oracle.folly_buffer(f["buffer_size"])
+    offs = np.array([v["offset"] for v in f["vectors"]], np.uint64)
+    lens = np.array([v["length"] for v in f["vectors"]], np.uint32)
+    got = _run_device(engine, fb, offs, lens)
+    assert [int(x) for x in got] == [v["crc"] for v in f["vectors"]]
+    # stitching (rocksdb/util/crc32c_test.cc:111-119) through the init column
+    half = lens // 2
+    first = _run_device(engine, fb, offs, half)
+    got = _run_device(engine, fb, offs + half, lens - half, inits=first)
+    assert [int(x) for x in got] == [v["crc"] for v in f["vectors"]]
+
+
+def test_small_spans_exhaustive(engine, oracle):
+    rng = np.random.default_rng(5)
+    buf = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    offs, lens, inits = [], [], []
+    for n in range(0, 301):
+        for o in range(0, 48):
+            offs.append(1024 + o + 7 * n)
+            lens.append(n)
+            inits.append(int(rng.integers(0, 2**32)) if (n + o) % 2 else 0)
+    offs, lens, inits = (np.array(offs, np.uint64), np.array(lens, np.uint32),
+                         np.array(inits, np.uint32))
+    got = _run_device(engine, buf, offs, lens, inits)
+    np.testing.assert_array_equal(got, oracle.batch(buf, offs, lens, inits))
+
+
+def test_segment_and_large_spans(engine, oracle):
+    rng = np.random.default_rng(9)
+    buf = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    lens = [65535, 65536, 65537, 65551, 65552, 65553, 65536 + 4097, 98304, 131071, 131072,
+            131073, 200003, 1 << 20, (1 << 20) + 3, (2 << 20) + 17]
+    offs, ln, ini = [], [], []
+    for n in lens:
+        for o in (0, 1, 8, 15, 16, 33):
+            offs.append(o)
+            ln.append(n)
+            ini.append(0 if o % 2 == 0 else 0xDEADBEEF)
+    offs, ln, ini = np.array(offs, np.uint64), np.array(ln, np.uint32), np.array(ini, np.uint32)
+    got = _run_device(engine, buf, offs, ln, ini)
+    np.testing.assert_array_equal(got, oracle.batch(buf, offs, ln, ini))
+
+
+def test_zipf_mixed_sst_packing(engine, oracle):
+    rng = np.random.default_rng(13)
+    buckets = np.array([512, 1024, 2048, 4096, 8192, 16384, 32768, 65536])
+    p = 1.0 / np.arange(1, 9) ** 0.99
+    p /= p.sum()
+    buf = rng.integers(0, 256, 48 << 20, dtype=np.uint8)
+    offs, lens, cur = [], [], 0
+    while True:
+        L = int(rng.choice(buckets, p=p))
+        n = L + int(rng.integers(0, L // 8 + 1))
+        if cur + n + 5 > buf.size:
+            break
+        offs.append(cur)
+        lens.append(n)
+        cur += n + 5
+    offs, lens = np.array(offs, np.uint64), np.array(lens, np.uint32)
+    got = _run_device(engine, buf, offs, lens)
+    np.testing.assert_array_equal(got, oracle.batch(buf, offs, lens))
+
+
+def test_full_size_4k_blocks(engine, oracle, reference):
+    """BASELINE configs[1]: 1 M x 4 KiB device-resident, device-generated."""
+    import torch
+    from tests.golden.common import splitmix64_bytes
+    nblk, bs, seed = 1 << 20, 4096, 0x4B10C5
+    dbuf = torch.empty(nblk * bs, dtype=torch.uint8, device="cuda:0")
+    engine.fill_splitmix64_device(dbuf, seed)
+    strided = _u32(engine.batch_strided_device(dbuf, bs, bs, nblk))
+    offs = torch.arange(nblk, dtype=torch.int64, device="cuda:0") * bs
+    lens = torch.full((nblk,), bs, dtype=torch.int32, device="cuda:0")
+    spans = _u32(engine.batch_device(dbuf, offs, lens))
+    np.testing.assert_array_equal(strided, spans)
+    host = dbuf.cpu().numpy()
+    assert np.array_equal(host[:4096], splitmix64_bytes(seed, 4096))  # fill rule
+    want = reference.batch(host, np.arange(nblk, dtype=np.uint64) * bs,
+                           np.full(nblk, bs, np.uint32), threads=8)
+    np.testing.assert_array_equal(spans, want)
+    sample = np.random.default_rng(0).choice(nblk, 2000, replace=False).astype(np.uint64)
+    np.testing.assert_array_equal(spans[sample],
+                                  oracle.batch(host, sample * bs, np.full(sample.size, bs, np.uint32)))
+    # size-independent property over the whole device buffer: chain all blocks
+    # pairwise, Extend(Extend(0, A), B) == Value(A||B)
+    pair = _u32(engine.batch_device(dbuf, offs[::2].contiguous(),
+                                    torch.full((nblk // 2,), 2 * bs, dtype=torch.int32,
+                                               device="cuda:0")))
+    chained = _u32(engine.batch_device(dbuf, offs[1::2].contiguous(), lens[1::2].contiguous(),
+                                       _t(spans[::2].copy())))
+    np.testing.assert_array_equal(pair, chained)
+    del dbuf
+
+
+def test_masked_strided_and_init(engine, oracle):
+    import torch
+    rng = np.random.default_rng(21)
+    buf = rng.integers(0, 256, 257 * 4096, dtype=np.uint8)
+    d = _t(buf)
+    for length, stride, init in ((4096, 4096, 0), (4097, 4101, 0x12345678), (100, 4096, 7)):
+        n = (buf.size - length) // stride
+        got = _u32(engine.batch_strided_device(d, stride, length, n, init=init, mask_output=True))
+        offs = np.arange(n, dtype=np.uint64) * stride
+        want = oracle.batch(buf, offs, np.full(n, length, np.uint32),
+                            np.full(n, init, np.uint32), mask=True)
+        np.testing.assert_array_equal(got, want)
+    torch.cuda.synchronize()
+
+
+def test_verify_blocks(engine, oracle):
+    """ReadBlock's check (kv/src/table/format.cc:91-99) on an SST-like buffer."""
+    rng = np.random.default_rng(17)
+    buf = np.zeros(6 << 20, np.uint8)
+    offs, lens, cur = [], [], 0
+    while cur + 4300 < buf.size:
+        n = int(rng.integers(4096, 4225))
+        buf[cur:cur + n] = rng.integers(0, 256, n, dtype=np.uint8)
+        buf[cur + n] = 0  # kNoCompression
+        crc = oracle.extend(0, buf, cur, n + 1)
+        m = int(oracle.lib.oracle_mask(crc))
+        buf[cur + n + 1:cur + n + 5] = np.frombuffer(m.to_bytes(4, "little"), np.uint8)
+        offs.append(cur)
+        lens.append(n)
+        cur += n + 5
+    offs, lens = np.array(offs, np.uint64), np.array(lens, np.uint32)
+    bad = rng.choice(offs.size, 25, replace=False)
+    for i, b in enumerate(bad):
+        where = int(offs[b]) + (int(rng.integers(0, lens[b] + 5)) if i % 2 else int(lens[b]) + 2)
+        buf[where] ^= 0x40
+    st = _t(np.zeros(offs.size, np.uint8))
+    engine.verify_device(_t(buf), _t(offs), _t(lens), st)
+    import torch
+    torch.cuda.synchronize()
+    status = st.cpu().numpy()
+    expect = np.ones(offs.size, np.uint8)
+    expect[bad] = 0
+    np.testing.assert_array_equal(status, expect)
+
+
+def test_batch_multi_one_device(oracle, golden_spans):
+    import torch  # noqa: F401
+    from wipdb_amd import batch_multi
+    g = golden_spans
+    got = batch_multi([0], g["buf"], g["offsets"], g["lengths"], g["inits"])
+    np.testing.assert_array_equal(got, g["crc"])
+
+
+def test_readstream_xor(engine):
+    rng = np.random.default_rng(2)
+    buf = rng.integers(0, 256, 64 * 4096, dtype=np.uint8)
+    got = _u32(engine.readstream_device(_t(buf), 4096, 4096, 64))
+    words = buf.view(np.uint32).reshape(64, 1024)
+    np.testing.assert_array_equal(got, np.bitwise_xor.reduce(words, axis=1))
+
+
+def test_async_requires_device_flag(engine):
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    assert lib.hcrc_batch_async(engine._ctx, 1, 1, 1, None, 1, 1, 0, None) == _lib.HCRC_ERR_INVALID
+
+
+def test_cpp_surface_drop_in_gpu(tmp_path):
+    exe = str(tmp_path / "test_surface")
+    libdir = os.path.join(REPO, "wipdb_amd", "lib")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "cpp", "test_surface.cc"), "-L", libdir,
+                    "-lhip_crc32c_batch", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr

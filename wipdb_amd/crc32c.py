@@ -1,0 +1,226 @@
+"""Python mirror of WipDB's crc32c surface and of the batch engine.
+
+Per-span functions mirror ``kv::crc32c`` (/root/reference/kv/src/util/crc32c.h):
+``extend`` (:24), ``value`` (:27-29), ``mask`` (:38-41), ``unmask`` (:44-47),
+``MASK_DELTA`` (:31), ``is_fast_crc32_supported`` (:19).  They run the
+library's host CPU path (crc32c_cpu.cc), as the reference's do.
+
+``Engine`` is the batch boundary: one context per GPU, spans handed to the
+gfx950 kernels through the C-ABI.  Inputs are either numpy arrays in host
+memory (staged through pinned buffers) or torch tensors already resident
+on the context's device (asynchronous, on the caller's stream).  Nothing
+here falls back to the CPU: a HIP failure raises ``HcrcError``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HcrcError, check
+
+MASK_DELTA = 0xA282EAD8
+
+
+def _ptr(a) -> int:
+    if a is None:
+        return 0
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())  # torch tensor
+
+
+def _as_bytes(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+# --------------------------------------------------------------------------
+# per-span surface (host CPU path), kv/src/util/crc32c.h
+# --------------------------------------------------------------------------
+def extend(init_crc: int, data) -> int:
+    """crc32c of concat(A, data) given init_crc = crc32c(A) (crc32c.h:21-24)."""
+    buf = _as_bytes(data)
+    return int(_lib.load().hcrc_cpu_extend(init_crc & 0xFFFFFFFF, _ptr(buf), buf.size))
+
+
+def value(data) -> int:
+    """crc32c of data (crc32c.h:27-29)."""
+    return extend(0, data)
+
+
+def mask(crc: int) -> int:
+    """Rotate right 15, add kMaskDelta (crc32c.h:38-41)."""
+    crc &= 0xFFFFFFFF
+    return (((crc >> 15) | (crc << 17)) + MASK_DELTA) & 0xFFFFFFFF
+
+
+def unmask(masked_crc: int) -> int:
+    """Inverse of mask (crc32c.h:44-47)."""
+    rot = (masked_crc - MASK_DELTA) & 0xFFFFFFFF
+    return ((rot >> 17) | (rot << 15)) & 0xFFFFFFFF
+
+
+def is_fast_crc32_supported() -> str:
+    """Same strings as crc32c.cc:467-492."""
+    return "Supported on x86" if _lib.load().hcrc_cpu_is_accelerated() else "Not supported on x86"
+
+
+def cpu_batch(base: np.ndarray, offsets, lengths, inits=None, mask_output=False,
+              threads: int = 1) -> np.ndarray:
+    """Host CPU batch (the library's own SSE4.2 path) -- not the GPU path."""
+    base = _as_bytes(base)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+    out = np.empty(off.size, dtype=np.uint32)
+    flags = HCRC_MASK_OUTPUT if mask_output else 0
+    check(_lib.load().hcrc_cpu_batch(_ptr(base), _ptr(off), _ptr(ln), _ptr(ini), _ptr(out),
+                                     off.size, flags, threads), "hcrc_cpu_batch")
+    return out
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = _lib.load().hcrc_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+# --------------------------------------------------------------------------
+# batch engine (GPU)
+# --------------------------------------------------------------------------
+class Engine:
+    """One hcrc context (device tables, stream, pinned staging) per GPU."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _lib.load()
+        ctx = ctypes.c_void_p()
+        check(self._lib.hcrc_ctx_create(device, ctypes.byref(ctx)), f"hcrc_ctx_create({device})")
+        self._ctx = ctx
+        self.device = device
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.hcrc_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return int(self._lib.hcrc_ctx_stream(self._ctx) or 0)
+
+    # -- host memory ------------------------------------------------------
+    def batch(self, base, offsets, lengths, inits=None, mask_output: bool = False) -> np.ndarray:
+        """Synchronous batch over host memory (pinned staging, H2D, kernel, D2H)."""
+        base = _as_bytes(base)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+        out = np.empty(off.size, dtype=np.uint32)
+        flags = HCRC_MASK_OUTPUT if mask_output else 0
+        check(self._lib.hcrc_batch(self._ctx, _ptr(base), _ptr(off), _ptr(ln), _ptr(ini),
+                                   _ptr(out), off.size, flags), "hcrc_batch")
+        return out
+
+    # -- device memory (torch tensors on this device) ----------------------
+    @staticmethod
+    def _stream_of(stream) -> int:
+        if stream is None:
+            import torch
+            return int(torch.cuda.current_stream().cuda_stream)
+        return int(stream)
+
+    def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
+                     mask_output: bool = False, stream=None):
+        """Asynchronous batch on device tensors; returns the uint32 out tensor
+        (int32 storage).  Enqueued on ``stream`` (default: torch's current)."""
+        import torch
+        n = int(offsets_t.numel())
+        if out_t is None:
+            out_t = torch.empty(n, dtype=torch.int32, device=base_t.device)
+        flags = HCRC_DEVICE_PTRS | (HCRC_MASK_OUTPUT if mask_output else 0)
+        check(self._lib.hcrc_batch_async(self._ctx, _ptr(base_t), _ptr(offsets_t), _ptr(lengths_t),
+                                         _ptr(inits_t), _ptr(out_t), n, flags,
+                                         self._stream_of(stream)), "hcrc_batch_async")
+        return out_t
+
+    def batch_strided_device(self, base_t, stride: int, length: int, count: int, init: int = 0,
+                             out_t=None, mask_output: bool = False, stream=None):
+        import torch
+        if out_t is None:
+            out_t = torch.empty(count, dtype=torch.int32, device=base_t.device)
+        flags = HCRC_DEVICE_PTRS | (HCRC_MASK_OUTPUT if mask_output else 0)
+        check(self._lib.hcrc_batch_strided_async(self._ctx, _ptr(base_t), stride, length,
+                                                 init & 0xFFFFFFFF, _ptr(out_t), count, flags,
+                                                 self._stream_of(stream)),
+              "hcrc_batch_strided_async")
+        return out_t
+
+    def verify_device(self, base_t, offsets_t, lengths_t, status_t=None, stream=None):
+        """ReadBlock's check on device blocks: status[i] = 1 iff the stored
+        masked crc at byte n+1 matches Value(block, n+1)."""
+        import torch
+        n = int(offsets_t.numel())
+        if status_t is None:
+            status_t = torch.empty(n, dtype=torch.uint8, device=base_t.device)
+        check(self._lib.hcrc_verify_async(self._ctx, _ptr(base_t), _ptr(offsets_t), _ptr(lengths_t),
+                                          _ptr(status_t), n, self._stream_of(stream)),
+              "hcrc_verify_async")
+        return status_t
+
+    def readstream_device(self, base_t, stride: int, length: int, count: int, out_t=None,
+                          stream=None):
+        import torch
+        if out_t is None:
+            out_t = torch.empty(count, dtype=torch.int32, device=base_t.device)
+        check(self._lib.hcrc_readstream_async(self._ctx, _ptr(base_t), stride, length,
+                                              _ptr(out_t), count, self._stream_of(stream)),
+              "hcrc_readstream_async")
+        return out_t
+
+    def fill_splitmix64_device(self, dst_t, seed: int, first_word: int = 0, stream=None):
+        """Fill a device tensor with the seeded splitmix64 stream."""
+        nbytes = int(dst_t.numel()) * dst_t.element_size()
+        check(self._lib.hcrc_fill_splitmix64_async(self._ctx, _ptr(dst_t), nbytes, seed,
+                                                   first_word, self._stream_of(stream)),
+              "hcrc_fill_splitmix64_async")
+        return dst_t
+
+    def sync(self, stream=None) -> None:
+        check(self._lib.hcrc_sync(self._ctx, stream or 0), "hcrc_sync")
+
+
+def batch_multi(devices: Sequence[int], base, offsets, lengths, inits=None,
+                mask_output: bool = False) -> np.ndarray:
+    """Host batch sharded by bytes over several GPUs (no collective)."""
+    lib = _lib.load()
+    base = _as_bytes(base)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+    out = np.empty(off.size, dtype=np.uint32)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    flags = HCRC_MASK_OUTPUT if mask_output else 0
+    check(lib.hcrc_batch_multi(devs, len(devices), _ptr(base), _ptr(off), _ptr(ln), _ptr(ini),
+                               _ptr(out), off.size, flags), "hcrc_batch_multi")
+    return out
+
+
+__all__ = [
+    "MASK_DELTA", "extend", "value", "mask", "unmask", "is_fast_crc32_supported",
+    "cpu_batch", "device_count", "Engine", "batch_multi", "HcrcError",
+]

@@ -1,0 +1,133 @@
+// crc32c_api.cc -- the C++ surface of include/wipdb/crc32c.h and the CPU
+// entry points of the C-ABI.
+//
+// kv::crc32c::Extend replaces kv/src/util/crc32c.cc:1225-1227 (and its
+// cpuid dispatch :1202-1224, here done lazily inside crc32c_cpu.cc, so there
+// is no static-initialisation-order hazard when Extend is called from
+// another translation unit's static constructor).  leveldb::crc32c::Extend
+// replaces leveldb/util/crc32c.cc:275-380.
+#include <stdint.h>
+
+#include <atomic>
+#include <mutex>
+#include <string>
+
+#include "../../include/hip_crc32c_batch.h"
+#include "../../include/wipdb/crc32c.h"
+#include "gf2_crc32c.h"
+
+namespace wipdb {
+namespace cpu {
+uint32_t Extend(uint32_t init_crc, const void* data, size_t n);
+bool IsAccelerated();
+void Batch(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+           const uint32_t* inits, uint32_t* out, size_t count, bool mask,
+           int threads);
+}  // namespace cpu
+}  // namespace wipdb
+
+namespace kv {
+namespace crc32c {
+
+std::string IsFastCrc32Supported() {
+  // Same strings as the reference (kv/src/util/crc32c.cc:467-492).
+  return wipdb::cpu::IsAccelerated() ? "Supported on x86" : "Not supported on x86";
+}
+
+uint32_t Extend(uint32_t init_crc, const char* data, size_t n) {
+  return wipdb::cpu::Extend(init_crc, data, n);
+}
+
+}  // namespace crc32c
+}  // namespace kv
+
+namespace leveldb {
+namespace crc32c {
+uint32_t Extend(uint32_t init_crc, const char* data, size_t n) {
+  return wipdb::cpu::Extend(init_crc, data, n);
+}
+}  // namespace crc32c
+}  // namespace leveldb
+
+namespace wipdb {
+namespace crc32c {
+
+namespace {
+std::atomic<size_t> g_min_gpu_batch{64};
+std::atomic<uint64_t> g_gpu_batches{0}, g_cpu_batches{0};
+std::atomic<int> g_last_error{0};
+std::mutex g_mu;
+hcrc_ctx* g_ctx[64] = {nullptr};
+int g_ctx_rc[64] = {0};
+bool g_ctx_tried[64] = {false};
+
+int CtxFor(int device, hcrc_ctx** out) {
+  if (device < 0 || device >= 64) return HCRC_ERR_NO_DEVICE;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_ctx_tried[device]) {
+    g_ctx_tried[device] = true;
+    g_ctx_rc[device] = hcrc_ctx_create(device, &g_ctx[device]);
+  }
+  *out = g_ctx[device];
+  return g_ctx_rc[device];
+}
+}  // namespace
+
+int ExtendBatch(const char* base, const uint64_t* offsets, const uint32_t* lengths,
+                const uint32_t* inits, uint32_t* out, size_t count, bool mask,
+                BatchPolicy policy, int device) {
+  const int flags = mask ? HCRC_MASK_OUTPUT : 0;
+  if (policy != BatchPolicy::kCpuOnly &&
+      (policy == BatchPolicy::kGpuOnly || count >= g_min_gpu_batch.load())) {
+    hcrc_ctx* ctx = nullptr;
+    int rc = CtxFor(device, &ctx);
+    if (rc == HCRC_OK)
+      rc = hcrc_batch(ctx, base, offsets, lengths, inits, out, count, flags);
+    if (rc == HCRC_OK) {
+      ++g_gpu_batches;
+      return HCRC_OK;
+    }
+    if (policy == BatchPolicy::kGpuOnly) return rc;
+    g_last_error = rc;  // kAuto: stay infallible, like Extend
+  }
+  wipdb::cpu::Batch(reinterpret_cast<const uint8_t*>(base), offsets, lengths, inits,
+                    out, count, mask, 1);
+  ++g_cpu_batches;
+  return HCRC_OK;
+}
+
+void SetMinGpuBatch(size_t spans) { g_min_gpu_batch = spans; }
+
+BatchStats GetBatchStats() {
+  BatchStats s;
+  s.gpu_batches = g_gpu_batches.load();
+  s.cpu_batches = g_cpu_batches.load();
+  s.last_error = g_last_error.load();
+  return s;
+}
+
+}  // namespace crc32c
+}  // namespace wipdb
+
+extern "C" {
+
+uint32_t hcrc_cpu_extend(uint32_t init_crc, const void* data, size_t n) {
+  return wipdb::cpu::Extend(init_crc, data, n);
+}
+
+int hcrc_cpu_batch(const void* base, const uint64_t* offsets,
+                   const uint32_t* lengths, const uint32_t* init_crcs,
+                   uint32_t* out_crcs, size_t count, int flags, int threads) {
+  if (count && (!base || !offsets || !lengths || !out_crcs)) return HCRC_ERR_INVALID;
+  if (flags & HCRC_DEVICE_PTRS) return HCRC_ERR_INVALID;
+  wipdb::cpu::Batch(static_cast<const uint8_t*>(base), offsets, lengths, init_crcs,
+                    out_crcs, count, (flags & HCRC_MASK_OUTPUT) != 0, threads);
+  return HCRC_OK;
+}
+
+int hcrc_cpu_is_accelerated(void) { return wipdb::cpu::IsAccelerated() ? 1 : 0; }
+
+uint32_t hcrc_mask(uint32_t crc) { return wipdb::gf2::Mask(crc); }
+uint32_t hcrc_unmask(uint32_t masked_crc) { return wipdb::gf2::Unmask(masked_crc); }
+
+}  // extern "C"

@@ -1,0 +1,547 @@
+// hcrc_api.cc -- host side of the hip_crc32c_batch C-ABI
+// (include/hip_crc32c_batch.h): contexts, table upload, launches, pinned
+// staging for host-resident batches, multi-GPU sharding.
+//
+// The kernels are in crc32c_kernels.hip; the CPU path in crc32c_cpu.cc.
+// No entry point here falls back to the CPU: every HIP failure is returned
+// as an HCRC_ERR_* code (DESIGN.md "Errors").
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/hip_crc32c_batch.h"
+#include "crc32c_device.h"
+#include "gf2_crc32c.h"
+
+namespace wipdb {
+namespace cpu {
+uint32_t Extend(uint32_t init_crc, const void* data, size_t n);
+bool IsAccelerated();
+void Batch(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+           const uint32_t* inits, uint32_t* out, size_t count, bool mask,
+           int threads);
+}  // namespace cpu
+namespace dev {
+__global__ void crc32c_spans_kernel(const uint8_t*, const uint64_t*,
+                                    const uint32_t*, const uint32_t*, uint32_t*,
+                                    uint64_t, uint32_t, const DevTables*);
+__global__ void crc32c_strided_kernel(const uint8_t*, uint64_t, uint32_t,
+                                      uint32_t, uint32_t*, uint64_t, uint32_t,
+                                      const DevTables*);
+__global__ void crc32c_verify_kernel(const uint8_t*, const uint64_t*,
+                                     const uint32_t*, uint8_t*, uint64_t,
+                                     const DevTables*);
+__global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*,
+                                  uint64_t);
+__global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
+}  // namespace dev
+}  // namespace wipdb
+
+using wipdb::dev::DevTables;
+
+namespace {
+
+constexpr size_t kSlotBytes = size_t(64) << 20;  // pinned staging per slot
+constexpr size_t kSlotSpans = size_t(1) << 18;   // descriptors per slot
+
+struct Slot {
+  uint8_t* h_data = nullptr;  // pinned
+  uint64_t* h_off = nullptr;  // pinned
+  uint32_t* h_len = nullptr;
+  uint32_t* h_init = nullptr;
+  uint32_t* h_out = nullptr;
+  uint8_t* d_data = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_len = nullptr;
+  uint32_t* d_init = nullptr;
+  uint32_t* d_out = nullptr;
+  size_t cap_bytes = 0;
+  hipEvent_t done = nullptr;
+  // results still to be copied out to the caller once `done` fires
+  uint32_t* user_out = nullptr;
+  size_t n_out = 0;
+};
+
+}  // namespace
+
+struct hcrc_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  DevTables* d_tab = nullptr;
+  int num_cu = 0;
+  std::mutex mu;
+  Slot slots[2];
+  bool slots_ready = false;
+};
+
+namespace {
+
+#define HCRC_CHECK(expr)                                  \
+  do {                                                    \
+    hipError_t e_ = (expr);                               \
+    if (e_ != hipSuccess) {                               \
+      return e_ == hipErrorOutOfMemory ? HCRC_ERR_NO_MEMORY \
+                                       : HCRC_ERR_HIP;    \
+    }                                                     \
+  } while (0)
+
+const wipdb::gf2::Tables& HostTables() {
+  static const wipdb::gf2::Tables* t = [] {
+    auto* x = new wipdb::gf2::Tables;
+    wipdb::gf2::BuildTables(x);
+    return x;
+  }();
+  return *t;
+}
+
+void BuildDevTables(DevTables* dt) {
+  const auto& T = HostTables();
+  memcpy(dt->t0, T.t[0], sizeof(dt->t0));
+  memcpy(dt->t1, T.t[1], sizeof(dt->t1));
+  for (uint32_t j = 0; j < wipdb::dev::kNumShift; ++j)
+    wipdb::gf2::BuildShiftTable(uint64_t(16) << j, dt->shift[j]);
+  for (int i = 0; i < 256; ++i) dt->inv_top[i] = T.inv_top[i];
+  memcpy(dt->head0, T.head0, sizeof(dt->head0));
+}
+
+int LaunchGrid(hcrc_ctx* ctx, size_t count) {
+  size_t need = (count + wipdb::dev::kWaves - 1) / wipdb::dev::kWaves;
+  size_t g = std::min<size_t>(need, size_t(ctx->num_cu));
+  return static_cast<int>(std::max<size_t>(g, 1));
+}
+
+int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off,
+                const uint32_t* len, const uint32_t* init, uint32_t* out,
+                size_t count, int flags, hipStream_t st) {
+  if (count == 0) return HCRC_OK;
+  hipLaunchKernelGGL(wipdb::dev::crc32c_spans_kernel, dim3(LaunchGrid(ctx, count)),
+                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+                     static_cast<const uint8_t*>(base), off, len, init, out,
+                     static_cast<uint64_t>(count),
+                     static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_tab);
+  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+}
+
+hipStream_t StreamOf(hcrc_ctx* ctx, void* stream) {
+  return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+int EnsureSlots(hcrc_ctx* ctx) {
+  if (ctx->slots_ready) return HCRC_OK;
+  for (Slot& s : ctx->slots) {
+    HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_data), kSlotBytes));
+    HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_off), kSlotSpans * 8));
+    HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_len), kSlotSpans * 4));
+    HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_init), kSlotSpans * 4));
+    HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), kSlotSpans * 4));
+    HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_data), kSlotBytes));
+    HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_off), kSlotSpans * 8));
+    HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_len), kSlotSpans * 4));
+    HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_init), kSlotSpans * 4));
+    HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_out), kSlotSpans * 4));
+    HCRC_CHECK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    s.cap_bytes = kSlotBytes;
+  }
+  ctx->slots_ready = true;
+  return HCRC_OK;
+}
+
+int GrowSlot(Slot& s, size_t bytes) {
+  if (bytes <= s.cap_bytes) return HCRC_OK;
+  HCRC_CHECK(hipHostFree(s.h_data));
+  HCRC_CHECK(hipFree(s.d_data));
+  s.h_data = nullptr;
+  s.d_data = nullptr;
+  HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_data), bytes));
+  HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_data), bytes));
+  s.cap_bytes = bytes;
+  return HCRC_OK;
+}
+
+// Wait for a slot's previous piece and hand its results to the caller.
+int DrainSlot(Slot& s) {
+  if (!s.user_out) return HCRC_OK;
+  HCRC_CHECK(hipEventSynchronize(s.done));
+  memcpy(s.user_out, s.h_out, s.n_out * 4);
+  s.user_out = nullptr;
+  s.n_out = 0;
+  return HCRC_OK;
+}
+
+// Copy spans [lo, hi) into the slot's pinned buffer, keeping each span's
+// address mod 16 (so aligned blocks stay on the aligned fast path).
+void PackSpans(Slot& s, const uint8_t* base, const uint64_t* offsets,
+               const uint32_t* lengths, const uint32_t* inits, size_t lo,
+               size_t hi, size_t* used_bytes) {
+  size_t cur = 0;
+  for (size_t i = lo; i < hi; ++i) {
+    const uint8_t* src = base + offsets[i];
+    cur = ((cur + 15) & ~size_t(15)) + (reinterpret_cast<uintptr_t>(src) & 15);
+    s.h_off[i - lo] = cur;
+    s.h_len[i - lo] = lengths[i];
+    s.h_init[i - lo] = inits ? inits[i] : 0u;
+    cur += lengths[i];
+  }
+  *used_bytes = cur;
+  // the byte copy itself, split over a few threads for big pieces
+  const size_t n = hi - lo;
+  auto copy = [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i)
+      memcpy(s.h_data + s.h_off[i], base + offsets[lo + i], s.h_len[i]);
+  };
+  if (cur < (size_t(8) << 20) || n < 64) {
+    copy(0, n);
+  } else {
+    const int nt = 8;
+    std::vector<std::thread> pool;
+    const size_t per = (n + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+      size_t a = per * t, b = std::min(n, a + per);
+      if (a >= b) break;
+      pool.emplace_back(copy, a, b);
+    }
+    for (auto& th : pool) th.join();
+  }
+}
+
+size_t PackedBytes(const uint64_t* offsets, const uint32_t* lengths,
+                   const uint8_t* base, size_t i) {
+  (void)offsets;
+  (void)base;
+  return size_t(lengths[i]) + 32;
+}
+
+int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
+              const uint32_t* lengths, const uint32_t* inits, uint32_t* out,
+              size_t count, int flags) {
+  int rc = EnsureSlots(ctx);
+  if (rc) return rc;
+  size_t i = 0;
+  int k = 0;
+  while (i < count) {
+    Slot& s = ctx->slots[k];
+    rc = DrainSlot(s);
+    if (rc) return rc;
+    // piece = spans [i, j) fitting the slot
+    size_t bytes = 0, j = i;
+    while (j < count && j - i < kSlotSpans) {
+      size_t b = PackedBytes(offsets, lengths, base, j);
+      if (j > i && bytes + b > s.cap_bytes) break;
+      bytes += b;
+      ++j;
+    }
+    rc = GrowSlot(s, bytes);
+    if (rc) return rc;
+    size_t used = 0;
+    PackSpans(s, base, offsets, lengths, inits, i, j, &used);
+    const size_t n = j - i;
+    HCRC_CHECK(hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice,
+                              ctx->stream));
+    HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice,
+                              ctx->stream));
+    HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice,
+                              ctx->stream));
+    HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice,
+                              ctx->stream));
+    rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, s.d_init, s.d_out, n,
+                     flags, ctx->stream);
+    if (rc) return rc;
+    HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    HCRC_CHECK(hipEventRecord(s.done, ctx->stream));
+    s.user_out = out + i;
+    s.n_out = n;
+    i = j;
+    k ^= 1;
+  }
+  for (Slot& s : ctx->slots) {
+    rc = DrainSlot(s);
+    if (rc) return rc;
+  }
+  return HCRC_OK;
+}
+
+std::mutex g_ctx_mu;
+std::map<int, hcrc_ctx*>& SharedCtxs() {
+  static auto* m = new std::map<int, hcrc_ctx*>;
+  return *m;
+}
+
+int SharedCtx(int device, hcrc_ctx** out) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto& m = SharedCtxs();
+  auto it = m.find(device);
+  if (it != m.end()) {
+    *out = it->second;
+    return HCRC_OK;
+  }
+  int rc = hcrc_ctx_create(device, out);
+  if (rc) return rc;
+  m[device] = *out;
+  return HCRC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hcrc_abi_version(void) { return HCRC_ABI_VERSION; }
+
+int hcrc_device_count(int* count) {
+  if (!count) return HCRC_ERR_INVALID;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    *count = 0;
+    return HCRC_ERR_NO_DEVICE;
+  }
+  *count = n;
+  return HCRC_OK;
+}
+
+const char* hcrc_strerror(int code) {
+  switch (code) {
+    case HCRC_OK: return "ok";
+    case HCRC_ERR_INVALID: return "invalid argument";
+    case HCRC_ERR_NO_DEVICE: return "no HIP device";
+    case HCRC_ERR_NO_MEMORY: return "out of memory";
+    case HCRC_ERR_HIP: return "HIP runtime error";
+    case HCRC_ERR_LAUNCH: return "kernel launch failed";
+    case HCRC_ERR_MISMATCH: return "checksum mismatch";
+    default: return "unknown error";
+  }
+}
+
+int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
+  if (!out_ctx) return HCRC_ERR_INVALID;
+  *out_ctx = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+    return HCRC_ERR_NO_DEVICE;
+  std::unique_ptr<hcrc_ctx> ctx(new hcrc_ctx);
+  ctx->device = device;
+  HCRC_CHECK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HCRC_CHECK(hipGetDeviceProperties(&prop, device));
+  ctx->num_cu = prop.multiProcessorCount;
+  HCRC_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  const unsigned lds = wipdb::dev::kLdsBytes;
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::dev::crc32c_spans_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::dev::crc32c_strided_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::dev::crc32c_verify_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  std::unique_ptr<DevTables> ht(new DevTables);
+  BuildDevTables(ht.get());
+  HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_tab), sizeof(DevTables)));
+  HCRC_CHECK(hipMemcpy(ctx->d_tab, ht.get(), sizeof(DevTables),
+                       hipMemcpyHostToDevice));
+  *out_ctx = ctx.release();
+  return HCRC_OK;
+}
+
+int hcrc_ctx_destroy(hcrc_ctx* ctx) {
+  if (!ctx) return HCRC_ERR_INVALID;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    auto& m = SharedCtxs();
+    auto it = m.find(ctx->device);
+    if (it != m.end() && it->second == ctx) m.erase(it);
+  }
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (Slot& s : ctx->slots) {
+    if (s.h_data) (void)hipHostFree(s.h_data);
+    if (s.h_off) (void)hipHostFree(s.h_off);
+    if (s.h_len) (void)hipHostFree(s.h_len);
+    if (s.h_init) (void)hipHostFree(s.h_init);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.d_data) (void)hipFree(s.d_data);
+    if (s.d_off) (void)hipFree(s.d_off);
+    if (s.d_len) (void)hipFree(s.d_len);
+    if (s.d_init) (void)hipFree(s.d_init);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  if (ctx->d_tab) (void)hipFree(ctx->d_tab);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return HCRC_OK;
+}
+
+void* hcrc_ctx_stream(hcrc_ctx* ctx) { return ctx ? ctx->stream : nullptr; }
+int hcrc_ctx_device(hcrc_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets,
+               const uint32_t* lengths, const uint32_t* init_crcs,
+               uint32_t* out_crcs, size_t count, int flags) {
+  if (!ctx || (count && (!base || !offsets || !lengths || !out_crcs)))
+    return HCRC_ERR_INVALID;
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT)) return HCRC_ERR_INVALID;
+  if (count == 0) return HCRC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HCRC_CHECK(hipSetDevice(ctx->device));
+  if (flags & HCRC_DEVICE_PTRS) {
+    int rc = LaunchSpans(ctx, base, offsets, lengths, init_crcs, out_crcs, count,
+                         flags, ctx->stream);
+    if (rc) return rc;
+    HCRC_CHECK(hipStreamSynchronize(ctx->stream));
+    return HCRC_OK;
+  }
+  return BatchHost(ctx, static_cast<const uint8_t*>(base), offsets, lengths,
+                   init_crcs, out_crcs, count, flags);
+}
+
+int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
+                     const uint32_t* d_lengths, const uint32_t* d_init_crcs,
+                     uint32_t* d_out_crcs, size_t count, int flags,
+                     void* stream) {
+  if (!ctx || !(flags & HCRC_DEVICE_PTRS)) return HCRC_ERR_INVALID;
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT)) return HCRC_ERR_INVALID;
+  if (count && (!d_base || !d_offsets || !d_lengths || !d_out_crcs))
+    return HCRC_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HCRC_CHECK(hipSetDevice(ctx->device));
+  return LaunchSpans(ctx, d_base, d_offsets, d_lengths, d_init_crcs, d_out_crcs,
+                     count, flags, StreamOf(ctx, stream));
+}
+
+int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
+                             uint32_t length, uint32_t init_crc,
+                             uint32_t* d_out_crcs, size_t count, int flags,
+                             void* stream) {
+  if (!ctx || !(flags & HCRC_DEVICE_PTRS)) return HCRC_ERR_INVALID;
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT)) return HCRC_ERR_INVALID;
+  if (count && (!d_base || !d_out_crcs)) return HCRC_ERR_INVALID;
+  if (count == 0) return HCRC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HCRC_CHECK(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(wipdb::dev::crc32c_strided_kernel,
+                     dim3(LaunchGrid(ctx, count)), dim3(wipdb::dev::kThreads),
+                     wipdb::dev::kLdsBytes, StreamOf(ctx, stream),
+                     static_cast<const uint8_t*>(d_base), stride, length, init_crc,
+                     d_out_crcs, static_cast<uint64_t>(count),
+                     static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_tab);
+  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+}
+
+int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
+                      const uint32_t* d_lengths, uint8_t* d_status, size_t count,
+                      void* stream) {
+  if (!ctx) return HCRC_ERR_INVALID;
+  if (count && (!d_base || !d_offsets || !d_lengths || !d_status))
+    return HCRC_ERR_INVALID;
+  if (count == 0) return HCRC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HCRC_CHECK(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(wipdb::dev::crc32c_verify_kernel, dim3(LaunchGrid(ctx, count)),
+                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes,
+                     StreamOf(ctx, stream), static_cast<const uint8_t*>(d_base),
+                     d_offsets, d_lengths, d_status, static_cast<uint64_t>(count),
+                     ctx->d_tab);
+  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+}
+
+int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
+                          uint32_t length, uint32_t* d_out, size_t count,
+                          void* stream) {
+  if (!ctx || (count && (!d_base || !d_out)) || (length & 15))
+    return HCRC_ERR_INVALID;
+  if (count == 0) return HCRC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HCRC_CHECK(hipSetDevice(ctx->device));
+  // same geometry as the CRC kernels, no LDS tables
+  hipLaunchKernelGGL(wipdb::dev::readstream_kernel, dim3(LaunchGrid(ctx, count)),
+                     dim3(wipdb::dev::kThreads), 0, StreamOf(ctx, stream),
+                     static_cast<const uint8_t*>(d_base), stride, length, d_out,
+                     static_cast<uint64_t>(count));
+  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+}
+
+int hcrc_fill_splitmix64_async(hcrc_ctx* ctx, void* d_dst, uint64_t nbytes,
+                               uint64_t seed, uint64_t first_word, void* stream) {
+  if (!ctx || (nbytes && !d_dst) || (nbytes & 7) ||
+      (reinterpret_cast<uintptr_t>(d_dst) & 7))
+    return HCRC_ERR_INVALID;
+  if (nbytes == 0) return HCRC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HCRC_CHECK(hipSetDevice(ctx->device));
+  const uint64_t nwords = nbytes / 8;
+  const int grid = static_cast<int>(std::min<uint64_t>((nwords + 255) / 256,
+                                                       uint64_t(ctx->num_cu) * 16));
+  hipLaunchKernelGGL(wipdb::dev::fill_splitmix64_kernel, dim3(grid), dim3(256), 0,
+                     StreamOf(ctx, stream), static_cast<uint64_t*>(d_dst), nwords,
+                     first_word, seed);
+  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+}
+
+int hcrc_sync(hcrc_ctx* ctx, void* stream) {
+  if (!ctx) return HCRC_ERR_INVALID;
+  HCRC_CHECK(hipSetDevice(ctx->device));
+  HCRC_CHECK(hipStreamSynchronize(StreamOf(ctx, stream)));
+  return HCRC_OK;
+}
+
+int hcrc_batch_multi(const int* devices, int ndev, const void* base,
+                     const uint64_t* offsets, const uint32_t* lengths,
+                     const uint32_t* init_crcs, uint32_t* out_crcs, size_t count,
+                     int flags) {
+  if (!devices || ndev <= 0 || (flags & HCRC_DEVICE_PTRS)) return HCRC_ERR_INVALID;
+  if (count && (!base || !offsets || !lengths || !out_crcs))
+    return HCRC_ERR_INVALID;
+  if (count == 0) return HCRC_OK;
+  // byte-balanced contiguous shards
+  uint64_t total = 0;
+  for (size_t i = 0; i < count; ++i) total += lengths[i] + 64;
+  std::vector<size_t> cut(ndev + 1, count);
+  cut[0] = 0;
+  uint64_t acc = 0;
+  int d = 1;
+  for (size_t i = 0; i < count && d < ndev; ++i) {
+    acc += lengths[i] + 64;
+    while (d < ndev && acc >= total * d / ndev) cut[d++] = i + 1;
+  }
+  std::vector<int> rcs(ndev, HCRC_OK);
+  std::vector<std::thread> pool;
+  for (int k = 0; k < ndev; ++k) {
+    const size_t lo = cut[k], hi = cut[k + 1];
+    if (lo >= hi) continue;
+    pool.emplace_back([&, k, lo, hi] {
+      hcrc_ctx* ctx = nullptr;
+      int rc = SharedCtx(devices[k], &ctx);
+      if (rc == HCRC_OK)
+        rc = hcrc_batch(ctx, base, offsets + lo, lengths + lo,
+                        init_crcs ? init_crcs + lo : nullptr, out_crcs + lo,
+                        hi - lo, flags & HCRC_MASK_OUTPUT);
+      rcs[k] = rc;
+    });
+  }
+  for (auto& th : pool) th.join();
+  for (int rc : rcs)
+    if (rc) return rc;
+  return HCRC_OK;
+}
+
+int hcrc_host_alloc(size_t bytes, void** out_ptr) {
+  if (!out_ptr) return HCRC_ERR_INVALID;
+  HCRC_CHECK(hipHostMalloc(out_ptr, bytes));
+  return HCRC_OK;
+}
+
+int hcrc_host_free(void* ptr) {
+  HCRC_CHECK(hipHostFree(ptr));
+  return HCRC_OK;
+}
+
+}  // extern "C"
