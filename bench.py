@@ -55,6 +55,9 @@ def parse():
                    help="target CPU time of the reference baseline sample")
     p.add_argument("--readstream", action="store_true",
                    help="also time the read-stream ceiling kernel")
+    p.add_argument("--stride", type=int, default=BLOCK,
+                   help="diagnostic: block stride (0 = every block reads the same 4 KiB, "
+                        "i.e. cache-resident compute ceiling); the headline uses 4096")
     return p.parse_args()
 
 
@@ -155,7 +158,7 @@ def main():
     data = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     eng.fill_splitmix64_device(data, SEED, first_word=first * BLOCK // 8, stream=stream.cuda_stream)
-    offs = torch.arange(nblk, dtype=torch.int64, device=dev) * BLOCK
+    offs = torch.arange(nblk, dtype=torch.int64, device=dev) * a.stride
     lens = torch.full((nblk,), BLOCK, dtype=torch.int32, device=dev)
     out = torch.empty(nblk, dtype=torch.int32, device=dev)
 
@@ -163,7 +166,7 @@ def main():
         if a.mode == "spans":
             eng.batch_device(data, offs, lens, None, out, stream=stream.cuda_stream)
         else:
-            eng.batch_strided_device(data, BLOCK, BLOCK, nblk, 0, out, stream=stream.cuda_stream)
+            eng.batch_strided_device(data, a.stride, BLOCK, nblk, 0, out, stream=stream.cuda_stream)
 
     for _ in range(a.warmup):
         step()
@@ -240,7 +243,10 @@ def main():
         }
         if rs:
             line["readstream_ceiling"] = rs
-        if world == 1 and not a.no_cpu_baseline:
+        if a.stride != BLOCK:
+            line["config"]["diagnostic_stride"] = a.stride
+            line["metric"] += " [DIAGNOSTIC stride, not the headline]"
+        if world == 1 and not a.no_cpu_baseline and a.stride == BLOCK:
             gpu_crc = out.cpu().numpy().view(np.uint32)
             cb, par = cpu_baseline(SEED, gpu_crc, first, a.cpu_seconds)
             line["cpu_baseline"] = cb

@@ -93,7 +93,8 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets,
                uint32_t* out_crcs, size_t count, int flags);
 
 /* Asynchronous batch on device memory, enqueued on `stream` (a hipStream_t;
- * NULL = the context's stream).  Requires HCRC_DEVICE_PTRS in flags. */
+ * NULL = the HIP default stream, as in HIP itself; pass hcrc_ctx_stream(ctx)
+ * for the context's own stream).  Requires HCRC_DEVICE_PTRS in flags. */
 int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base,
                      const uint64_t* d_offsets, const uint32_t* d_lengths,
                      const uint32_t* d_init_crcs, uint32_t* d_out_crcs,
@@ -115,7 +116,7 @@ int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base,
                       const uint64_t* d_offsets, const uint32_t* d_lengths,
                       uint8_t* d_status, size_t count, void* stream);
 
-/* Wait for all work on `stream` (NULL = the context's stream). */
+/* Wait for all work on `stream` (NULL = the HIP default stream). */
 int hcrc_sync(hcrc_ctx* ctx, void* stream);
 
 /* Host-memory batch sharded over `ndev` devices by bytes, one host thread

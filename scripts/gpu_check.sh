@@ -26,6 +26,11 @@ for s in $STEPS; do
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    diag) run diag_s0 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --stride 0 &&
+          run diag_s0_strided 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --stride 0 --mode strided &&
+          run diag_small 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --blocks 16384 ;;
+    pmc_sq) run pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_sq2) run pmc_sq2 400 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s" ;;
   esac
 done

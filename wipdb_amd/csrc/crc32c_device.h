@@ -12,6 +12,7 @@ constexpr int kThreads = kWaves * 64;    // 1024 threads
 constexpr uint32_t kSegBytes = 65536;    // longest span one wave folds at once
 constexpr uint32_t kNumShift = 12;       // shift tables for 16*2^j bytes, j<12
 constexpr uint32_t kFlagMask = 0x2;      // == HCRC_MASK_OUTPUT
+constexpr int kChains = 4;               // independent CRC chains per lane
 
 // LDS map (bytes).
 //  [0, 64 KiB)   slicing-by-2 tables, 32 replicas: entry (b, u, lane) at

@@ -130,8 +130,12 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off,
   return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
 }
 
+// Async entry points take the caller's stream; NULL is the HIP default
+// (null) stream, as everywhere in HIP (torch's default stream is NULL too).
+// The context's own stream is available through hcrc_ctx_stream().
 hipStream_t StreamOf(hcrc_ctx* ctx, void* stream) {
-  return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  (void)ctx;
+  return static_cast<hipStream_t>(stream);
 }
 
 int EnsureSlots(hcrc_ctx* ctx) {
@@ -393,10 +397,11 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets,
   std::lock_guard<std::mutex> lk(ctx->mu);
   HCRC_CHECK(hipSetDevice(ctx->device));
   if (flags & HCRC_DEVICE_PTRS) {
+    // default stream: ordered after whatever the caller enqueued there
     int rc = LaunchSpans(ctx, base, offsets, lengths, init_crcs, out_crcs, count,
-                         flags, ctx->stream);
+                         flags, nullptr);
     if (rc) return rc;
-    HCRC_CHECK(hipStreamSynchronize(ctx->stream));
+    HCRC_CHECK(hipStreamSynchronize(nullptr));
     return HCRC_OK;
   }
   return BatchHost(ctx, static_cast<const uint8_t*>(base), offsets, lengths,
