@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build an experimental variant of the product library with extra kernel
+# defines:  scripts/build_variant.sh NAME -DFOO=1 ...
+# -> build/variants/NAME/libhip_crc32c_batch.so  (load it with WIPDB_HCRC_LIB)
+set -euo pipefail
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+NAME=$1; shift
+make -s -C "$ROOT/wipdb_amd/csrc" >/dev/null
+OUT="$ROOT/build/variants/$NAME"
+mkdir -p "$OUT"
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 "$@" \
+  -c -o "$OUT/crc32c_kernels.o" "$ROOT/wipdb_amd/csrc/crc32c_kernels.hip"
+O="$ROOT/build/obj"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libhip_crc32c_batch.so" \
+  "$OUT/crc32c_kernels.o" "$O/hcrc_api.o" "$O/crc32c_api.o" "$O/crc32c_cpu.o" -lpthread
+echo "$OUT/libhip_crc32c_batch.so"

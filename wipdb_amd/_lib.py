@@ -12,7 +12,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libhip_crc32c_batch.so")
+# WIPDB_HCRC_LIB: load another build of the same library (kernel experiments
+# compare variants in one GPU session); the default is the in-tree build.
+LIB_PATH = os.environ.get("WIPDB_HCRC_LIB") or os.path.join(_HERE, "lib", "libhip_crc32c_batch.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hip_crc32c_batch.h")
 
 HCRC_OK = 0

@@ -7,35 +7,47 @@
 // (kv/src/table/format.cc:91-93) do one block at a time.
 //
 // Design (DESIGN.md "Kernels"):
-//   * one span per wavefront.  The span's 16-byte chunks are split into
-//     64*K contiguous stripes ("virtual lanes"); lane l runs K independent
-//     CRC chains over K consecutive stripes, i.e. one contiguous run of
-//     K*c' chunks (16-byte loads; every byte of every line the wave fetches
-//     is used).  K chains per lane give the LDS-latency-bound byte scan the
-//     instruction-level parallelism it needs.
+//   * one span per wavefront, cut into 4 KiB segments of its 16-byte chunk
+//     grid.  A segment's 256 chunks are 64*K one-chunk stripes ("virtual
+//     lanes"): lane l runs K = 4 independent CRC chains over chunks l,
+//     64+l, 128+l, 192+l, so each 16-byte load instruction of the wave reads
+//     one contiguous KiB (fully coalesced).  The K chains give the
+//     LDS-latency-bound byte scan instruction-level parallelism.
 //   * CRC arithmetic is table-driven from LDS (CDNA4 has no carry-less
 //     multiply and this is a byte scan, not a contraction: no MFMA):
 //     slicing-by-2 tables replicated 32x so lane l always reads bank l&31 --
 //     every lookup is bank-conflict free -- and each lookup address is built
-//     by ONE v_perm_b32 (table byte | lane byte | table-select bit).
-//   * the 64*K stripe registers are folded by a GF(2) tree: first the K
-//     chains inside a lane, then a 6-level wavefront butterfly,
-//        reg(v) = shift(reg(v), stripe_bytes * 2^t) ^ reg(v + 2^t),
+//     by ONE v_perm_b32 (table byte | lane byte | region byte).
+//   * the 256 stripe registers are folded by a GF(2) tree: an in-lane Horner
+//     step over the 4 chains (shift by 1 KiB), then a 6-level wavefront
+//     butterfly (DPP row shifts, then v_readlane),
+//        reg(v) = shift(reg(v), 16 * 2^t bytes) ^ reg(v + 2^t),
 //     where shift by 16*2^j bytes is 4 lookups in a "multiply by
 //     x^(8*16*2^j) mod P" table (the carry-less combine of the reference's
 //     CombineCRC, crc32c.cc:640-657, done with tables).
 //   * unaligned starts: the first chunk's leading bytes are zeroed and the
 //     register injected there is pre-un-shifted (~init * x^(-8h)) so it
 //     equals ~init at the first real byte; the ragged end (< 16 bytes) is
-//     fed after the fold.  So any offset/length/init is bit-exact.
-//   * latency hiding: persistent grid (1 workgroup of 16 waves per CU, LDS =
-//     113 KiB), each wave walks its spans with a one-item software pipeline:
-//     the next item's chunk loads are issued before the current item is
-//     processed, and 64 span descriptors are fetched per vector load.
+//     fed after the fold.  Segments of one span are chained through init.
+//     So any offset/length/init is bit-exact.
+//   * latency hiding: persistent grid (1 workgroup of 16 waves per CU), each
+//     wave walks its spans' segments through a 3-slot register ring (two
+//     segments of loads in flight while one is computed); 64 span
+//     descriptors are fetched per vector load.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "crc32c_device.h"
+
+#ifndef WIPDB_FOLD_SELECT
+#define WIPDB_FOLD_SELECT 0
+#endif
+#ifndef WIPDB_OUTBUF
+#define WIPDB_OUTBUF 1
+#endif
+#ifndef WIPDB_RING_SLOTS
+#define WIPDB_RING_SLOTS 3
+#endif
 
 namespace wipdb {
 namespace dev {
@@ -51,11 +63,12 @@ __device__ __forceinline__ uint32_t lds_ld(uint32_t addr) {
   return *reinterpret_cast<l_u32*>(static_cast<uintptr_t>(addr));
 }
 
-constexpr uint32_t kSelT1B0 = 0x0c0c0004u;  // [s0.b0, x.b0, 0, 0] -> T1[x.b0]
-constexpr uint32_t kSelT0B1 = 0x0c0c0105u;  // [s0.b1, x.b1, 0, 0] -> T0[x.b1]
+// s0 = lane constant: byte0 = (lane&31)*4 (T1), byte1 = (lane&31)*4|0x80
+// (T0), byte2 = 0x01 (the 64 KiB region of the main tables).
+constexpr uint32_t kSelT1B0 = 0x0c060004u;  // [s0.b0, x.b0, s0.b2, 0] -> T1[x.b0]
+constexpr uint32_t kSelT0B1 = 0x0c060105u;  // [s0.b1, x.b1, s0.b2, 0] -> T0[x.b1]
 
 // Feed one little-endian 32-bit word into register r (slicing-by-2 twice).
-// s0 = lane constant: byte0 = (lane&31)*4 (T1), byte1 = (lane&31)*4|0x80 (T0).
 __device__ __forceinline__ uint32_t feed_word(uint32_t s0, uint32_t r, uint32_t w) {
   const uint32_t x = r ^ w;
   const uint32_t y = lds_ld(__builtin_amdgcn_perm(s0, x, kSelT1B0)) ^
@@ -102,30 +115,27 @@ __device__ __forceinline__ uint32_t row_shl(uint32_t v) {
 // Feed one byte (Sarwate step with this lane's T0 replica).
 __device__ __forceinline__ uint32_t feed_byte(uint32_t s0, uint32_t r, uint32_t b) {
   const uint32_t x = (r ^ b) & 0xffu;
-  return lds_ld((x << 8) | ((s0 >> 8) & 0xffu)) ^ (r >> 8);
+  return lds_ld(kLdsMain + ((x << 8) | ((s0 >> 8) & 0xffu))) ^ (r >> 8);
 }
 
-// r * x^(8 * 16 * 2^j) mod P: 4 lookups in shift table j.
-__device__ __forceinline__ uint32_t shift_pow2(uint32_t r, uint32_t j) {
-  const uint32_t base = kLdsShift + j * 4096u;
+// r * x^(8 * 16 * 2^J) mod P: 4 lookups in shift table J.  The table base
+// is a compile-time constant that lands in the ds_read offset field, so
+// each address is one v_lshlrev_b32_sdwa (byte select).
+template <uint32_t J>
+__device__ __forceinline__ uint32_t shift_pow2_c(uint32_t r) {
+  constexpr uint32_t base = kLdsShift + J * 4096u;
+  static_assert(base + 4096u <= 65536u, "ds_read offset field is 16 bits");
   return lds_ld(base + ((r & 0xffu) << 2)) ^
          lds_ld(base + 1024u + (((r >> 8) & 0xffu) << 2)) ^
          lds_ld(base + 2048u + (((r >> 16) & 0xffu) << 2)) ^
          lds_ld(base + 3072u + ((r >> 24) << 2));
 }
 
-// r * x^(8 * 16 * cp * 2^m): one table multiply per set bit of cp.
-__device__ __forceinline__ uint32_t shift_chunks(uint32_t r, uint32_t cp, uint32_t m) {
-  for (uint32_t b = 0; cp; cp >>= 1, ++b)
-    if (cp & 1u) r = shift_pow2(r, b + m);
-  return r;
-}
-
 // Un-feed h zero bytes (register that becomes r after h zero bytes).
 __device__ __forceinline__ uint32_t unshift_bytes(uint32_t s0, uint32_t r, uint32_t h) {
   for (uint32_t i = 0; i < h; ++i) {
     const uint32_t idx = lds_ld(kLdsInvTop + ((r >> 24) << 2));
-    const uint32_t t0 = lds_ld((idx << 8) | ((s0 >> 8) & 0xffu));
+    const uint32_t t0 = lds_ld(kLdsMain + ((idx << 8) | ((s0 >> 8) & 0xffu)));
     r = ((r ^ t0) << 8) | idx;
   }
   return r;
@@ -140,56 +150,74 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) {
 }
 
 // ---------------------------------------------------------------------------
-// Work items.  An item is one segment (<= kSegBytes) of one span; spans
-// longer than a segment are chained (init of segment k+1 = crc of segment k).
+// Segments.  A span is cut at 4 KiB boundaries of its 16-byte chunk grid:
+// segment = [start, start+n) with n = min(rest, 4096 - (start & 15)), so its
+// main region [start&~15, end&~15) holds at most 256 chunks = one chunk per
+// chain (64 lanes x K=4).  Every fold therefore uses the compile-time tables
+// of fold_wave_c2, and every segment is one load group.  Segments of one
+// span are chained: init of segment k+1 = crc of segment k (Extend).
 // All fields are wave-uniform.
 // ---------------------------------------------------------------------------
-struct Item {
-  uint64_t span;    // span index (>= count: no item)
-  uint64_t start;   // first byte (absolute address)
-  uint64_t rest;    // bytes of the span from `start` on (this + later segments)
-  uint64_t a0;      // 16-aligned start of the main region
-  uint32_t n;       // bytes in this segment
-  uint32_t cp;      // chunks per chain (0: no main region)
-  uint32_t pad;     // virtual chunks in front of the first real chunk
-  uint32_t h;       // bytes of chunk 0 in front of `start`
+constexpr uint32_t kSegChunks = 64u * kChains;  // 256 chunks = 4 KiB
+constexpr uint32_t kSlotFirst = 1u, kSlotLast = 2u, kSlotValid = 4u;
+
+// Segment geometry is kept in 32-bit offsets from the segment's 16-byte
+// aligned base: hn = h + n where h = start & 15.  The main region is
+// chunks [0, hn >> 4) of the base, the ragged tail is hn & 15 bytes after it.
+// (Uniform 64-bit compares are VALU compares whose result must be moved to
+// SCC; hipcc 7.2 mis-schedules that pattern next to another such compare, so
+// the wave loop avoids them.)
+struct Slot {
+  uint64_t start;  // first byte (absolute address)
+  uint32_t n;      // bytes in this segment
+  uint32_t init;   // span init (first segment only)
+  uint32_t flags;  // kSlotFirst | kSlotLast | kSlotValid
 };
 
-template <int K>
-__device__ __forceinline__ void item_geometry(Item& it) {
-  it.n = it.rest > kSegBytes ? kSegBytes : static_cast<uint32_t>(it.rest);
-  const uint64_t end = it.start + it.n;
-  const uint64_t a0 = it.start & ~uint64_t(15);
-  const uint64_t e0 = end & ~uint64_t(15);
-  it.a0 = a0;
-  it.h = static_cast<uint32_t>(it.start - a0);
-  if (e0 > it.start) {
-    const uint32_t cm = static_cast<uint32_t>((e0 - a0) >> 4);
-    const uint32_t v = 64u * K;
-    it.cp = (cm + v - 1u) / v;
-    it.pad = v * it.cp - cm;
-  } else {
-    it.cp = 0;
-    it.pad = 0;
-  }
+// Issues this lane's K = 4 chunk loads of segment s.  Virtual chunk
+// v = 64*k + lane (chain k of this lane) holds chunk q = v - pad of the main
+// region, so load k of the wave reads 64 consecutive chunks: one contiguous
+// KiB per instruction, fully coalesced.  Virtual chunks in front (q < 0)
+// read chunk 0 instead (always mapped: it holds the span's first byte); the
+// chains they feed are overwritten by the injection or zeroed before the
+// fold, so their data never matters.  Slots without a main region (or
+// invalid slots) load the KiB at `dummy` so that EVERY slot issues exactly
+// 4 vector loads: the ring stays regular.
+//
+// The issue is branch-free so hipcc's waitcnt pass sees the same 4 loads
+// per slot on every path and can leave the ring's other slots in flight.
+__device__ __forceinline__ void issue_seg(const Slot& s, uint32_t lane, const void* dummy,
+                                          u32x4 (&d)[4]) {
+  const uint32_t hn = static_cast<uint32_t>(s.start & 15u) + s.n;
+  const bool live = (s.flags & kSlotValid) && hn >= 16u;
+  const uint32_t pad = live ? kSegChunks - (hn >> 4) : 0u;
+  const uint64_t base = live ? (s.start & ~uint64_t(15)) : reinterpret_cast<uint64_t>(dummy);
+  const uint32_t step = live ? 64u : 0u;
+  // chunk q_k = max(64k + lane - pad, 0), branch-free
+  const uint32_t v0 = lane, v1 = lane + step, v2 = lane + 2u * step, v3 = lane + 3u * step;
+  const uint32_t q0 = v0 > pad ? v0 - pad : 0u;
+  const uint32_t q1 = v1 > pad ? v1 - pad : 0u;
+  const uint32_t q2 = v2 > pad ? v2 - pad : 0u;
+  const uint32_t q3 = v3 > pad ? v3 - pad : 0u;
+  g_u32x4* g = reinterpret_cast<g_u32x4*>(base);
+  d[0] = __builtin_nontemporal_load(g + q0);
+  d[1] = __builtin_nontemporal_load(g + q1);
+  d[2] = __builtin_nontemporal_load(g + q2);
+  d[3] = __builtin_nontemporal_load(g + q3);
 }
 
-// Loads chunk group i of item `it` for this lane: chunk i of each of its K
-// chains.  Virtual chunks in front of the span (q < 0) read chunk 0 instead
-// (always mapped: it holds the span's first byte); the chains they feed are
-// overwritten by the injection or zeroed before the fold, so their data
-// never matters and the loads need no predicate.
-template <int K>
-__device__ __forceinline__ void load_group(const Item& it, uint32_t i, uint32_t lane,
-                                           u32x4 (&d)[K]) {
-  const int32_t q0 = static_cast<int32_t>(lane * K * it.cp + i) -
-                     static_cast<int32_t>(it.pad);
-  g_u32x4* cp = reinterpret_cast<g_u32x4*>(it.a0);
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int32_t q = q0 + k * static_cast<int32_t>(it.cp);
-    d[k] = __builtin_nontemporal_load(cp + (q > 0 ? q : 0));
-  }
+// The 16 bytes at a 16-byte aligned address `p` (uniform) through the
+// scalar cache: the ragged tail of a segment.  The wait is inside the asm,
+// so the vector-memory counter -- and the load ring -- is never drained.
+__device__ __forceinline__ void tail_chunk(uint64_t p, uint32_t (&t)[4]) {
+  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+  u32x4s v;
+  // early-clobber: the destination must not overlap the address registers
+  asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(v) : "s"(p) : "memory");
+  t[0] = v.x;
+  t[1] = v.y;
+  t[2] = v.z;
+  t[3] = v.w;
 }
 
 // ---------------------------------------------------------------------------
@@ -220,7 +248,7 @@ struct DescSource {
       c_init = inits ? __builtin_nontemporal_load(inits + s) : 0u;
     }
   }
-  __device__ __forceinline__ void get(uint32_t j, uint64_t& start, uint64_t& len,
+  __device__ __forceinline__ void get(uint32_t j, uint64_t& start, uint32_t& len,
                                       uint32_t& init) const {
     const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c_off), j);
     const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(c_off >> 32), j);
@@ -228,14 +256,17 @@ struct DescSource {
     len = __builtin_amdgcn_readlane(c_len, j);
     init = __builtin_amdgcn_readlane(c_init, j);
   }
+  // Descriptor of span s, the wave's next span (spans are visited in order,
+  // `stride` apart): the cache index advances by one, no division.
+  uint32_t cj;
   __device__ __forceinline__ void desc(uint64_t s, uint64_t stride, uint32_t lane,
-                                       uint64_t& start, uint64_t& len, uint32_t& init) {
-    uint64_t j = (s - cache_first) / stride;
-    if (j >= 64) {
+                                       uint64_t& start, uint32_t& len, uint32_t& init) {
+    if (cj >= 64u) {
       fetch(s, stride, lane);
-      j = 0;
+      cj = 0u;
     }
-    get(static_cast<uint32_t>(j), start, len, init);
+    get(cj, start, len, init);
+    ++cj;
   }
 };
 
@@ -246,7 +277,7 @@ struct StridedSource {
   uint32_t init;
   uint64_t count;
   __device__ __forceinline__ void desc(uint64_t s, uint64_t, uint32_t, uint64_t& start,
-                                       uint64_t& len, uint32_t& ini) const {
+                                       uint32_t& len, uint32_t& ini) const {
     start = reinterpret_cast<uint64_t>(base) + s * stride_bytes;
     len = length;
     ini = init;
@@ -257,179 +288,271 @@ struct StridedSource {
 // The wave loop.  out(span, crc, lane) is called once per span with the
 // finished crc (uniform).
 // ---------------------------------------------------------------------------
-// Fold the 64*K stripe registers of a wave into the span register (uniform).
-// r[k] of lane l covers virtual stripe l*K+k of cp chunks.  In-lane levels
-// first, then the wavefront butterfly: DPP row shifts for partners 1..8
-// lanes away, v_readlane for 16 and 32.  Shift tables of 16*2^j bytes.
+// Fold the 64*K one-chunk stripe registers of a wave into the segment
+// register (uniform).  r[k] of lane l covers chunk 64k + l, i.e. sits
+// (3-k)*1 KiB + (63-l)*16 bytes before the segment end.  In-lane Horner over
+// k first (shift by 1 KiB), then the wavefront butterfly over lanes: DPP row
+// shifts for partners 1..8 lanes away, v_readlane for 16 and 32.  All table
+// indices are compile-time constants (shift by 16*2^J bytes).
 template <int K>
-__device__ __forceinline__ uint32_t fold_wave(uint32_t (&r)[K], uint32_t cp, uint32_t lane) {
-  constexpr uint32_t kLogK = K == 1 ? 0 : (K == 2 ? 1 : (K == 4 ? 2 : 3));
-#pragma unroll
-  for (uint32_t m = 0, w = 1; w < K; ++m, w <<= 1) {
-#pragma unroll
-    for (uint32_t k = 0; k + w < K; k += 2 * w) r[k] = shift_chunks(r[k], cp, m) ^ r[k + w];
-  }
-  uint32_t v = r[0];
+__device__ __forceinline__ uint32_t fold_wave_c2(uint32_t (&r)[K], uint32_t lane) {
+  static_assert(K == 4, "the fold is written for 4 chains per lane");
+  uint32_t v = shift_pow2_c<6>(r[0]) ^ r[1];
+  v = shift_pow2_c<6>(v) ^ r[2];
+  v = shift_pow2_c<6>(v) ^ r[3];
+#if WIPDB_FOLD_SELECT
+  // every lane computes every level (no exec-mask regions); the partner
+  // value is only kept where the level applies
   uint32_t p = row_shl<1>(v);
-  if ((lane & 1u) == 0u) v = shift_chunks(v, cp, kLogK + 0) ^ p;
+  uint32_t t = shift_pow2_c<0>(v) ^ p;
+  v = (lane & 1u) == 0u ? t : v;
   p = row_shl<2>(v);
-  if ((lane & 3u) == 0u) v = shift_chunks(v, cp, kLogK + 1) ^ p;
+  t = shift_pow2_c<1>(v) ^ p;
+  v = (lane & 3u) == 0u ? t : v;
   p = row_shl<4>(v);
-  if ((lane & 7u) == 0u) v = shift_chunks(v, cp, kLogK + 2) ^ p;
+  t = shift_pow2_c<2>(v) ^ p;
+  v = (lane & 7u) == 0u ? t : v;
   p = row_shl<8>(v);
-  if ((lane & 15u) == 0u) v = shift_chunks(v, cp, kLogK + 3) ^ p;
+  t = shift_pow2_c<3>(v) ^ p;
+  v = (lane & 15u) == 0u ? t : v;
   const uint32_t g16 = __builtin_amdgcn_readlane(v, 16);
   const uint32_t g48 = __builtin_amdgcn_readlane(v, 48);
-  if ((lane & 31u) == 0u) v = shift_chunks(v, cp, kLogK + 4) ^ (lane ? g48 : g16);
+  t = shift_pow2_c<4>(v) ^ (lane ? g48 : g16);
+  v = (lane & 31u) == 0u ? t : v;
+#else
+  uint32_t p = row_shl<1>(v);
+  if ((lane & 1u) == 0u) v = shift_pow2_c<0>(v) ^ p;
+  p = row_shl<2>(v);
+  if ((lane & 3u) == 0u) v = shift_pow2_c<1>(v) ^ p;
+  p = row_shl<4>(v);
+  if ((lane & 7u) == 0u) v = shift_pow2_c<2>(v) ^ p;
+  p = row_shl<8>(v);
+  if ((lane & 15u) == 0u) v = shift_pow2_c<3>(v) ^ p;
+  const uint32_t g16 = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t g48 = __builtin_amdgcn_readlane(v, 48);
+  if ((lane & 31u) == 0u) v = shift_pow2_c<4>(v) ^ (lane ? g48 : g16);
+#endif
   const uint32_t g0 = __builtin_amdgcn_readlane(v, 0);
   const uint32_t g32 = __builtin_amdgcn_readlane(v, 32);
-  return uni(shift_chunks(g0, cp, kLogK + 5) ^ g32);
+  return uni(shift_pow2_c<5>(g0) ^ g32);
 }
 
-template <int K, typename Src, typename Out>
-__device__ __forceinline__ void run_waves(Src& src, uint64_t first_span, uint64_t span_stride,
-                                          Out out) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t l4 = (threadIdx.x & 31u) * 4u;
-  const uint32_t s0 = l4 | ((l4 | 0x80u) << 8);
-  if (first_span >= src.count) return;
-  Item it;
-  uint32_t it_init;
-  it.span = first_span;
-  src.desc(it.span, span_stride, lane, it.start, it.rest, it_init);
-  item_geometry<K>(it);
+// Walks the wave's spans (first_span, first_span + stride, ...) and emits
+// their segments in order -- the load side of the pipeline.
+template <typename Src>
+struct SegCursor {
+  uint64_t span, start, stride;
+  uint32_t rest, init, first, left;  // left: spans not yet started, incl. this one
 
-  u32x4 cur[K], nxt[K];
-  if (it.cp) load_group<K>(it, 0, lane, cur);
-
-  for (;;) {
-    // next item (computed now so its first loads can be issued early)
-    Item nx;
-    uint32_t nx_init = 0;
-    if (it.rest > it.n) {
-      nx = it;
-      nx.start = it.start + it.n;
-      nx.rest = it.rest - it.n;
+  __device__ __forceinline__ void begin(Src& src, uint64_t s, uint64_t str, uint32_t lane) {
+    stride = str;
+    span = s;
+    left = static_cast<uint32_t>((src.count - s + str - 1) / str);  // s < count
+    first = 1u;
+    src.desc(s, stride, lane, start, rest, init);
+  }
+  __device__ __forceinline__ Slot next(Src& src, uint32_t lane) {
+    // every field defined on every path: an undef field read by issue_seg
+    // lets LLVM substitute another slot's value at the ring's merge points
+    Slot sl{0, 0, 0, 0};
+    if (left == 0u) return sl;
+    const uint32_t room = 4096u - static_cast<uint32_t>(start & 15u);
+    const bool last = rest <= room;
+    const uint32_t n = last ? rest : room;
+    sl.start = start;
+    sl.n = n;
+    sl.init = init;
+    sl.flags = kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u);
+    if (last) {
+      span += stride;
+      first = 1u;
+      --left;
+      if (left != 0u) src.desc(span, stride, lane, start, rest, init);
     } else {
-      nx.span = it.span + span_stride;
-      if (nx.span < src.count) src.desc(nx.span, span_stride, lane, nx.start, nx.rest, nx_init);
+      start += n;
+      rest -= n;
+      first = 0u;
     }
-    const bool nx_valid = nx.span < src.count;
-    if (nx_valid) item_geometry<K>(nx);
+    return sl;
+  }
+};
 
-    uint32_t reg;  // register after the main region (or ~init if none)
-    const uint32_t cp = it.cp;
-    const uint64_t end = it.start + it.n;
-    if (cp && it.h == 0 && it.pad == 0 && (end & 15u) == 0) {
-      // ---- fast path: aligned start, whole stripes, no ragged end ----
-      // The register ~init enters at lane 0, chain 0, before any byte.
-      uint32_t r[K];
+// Processes one segment whose chunks are in d (already waited for).
+// Returns true when the segment completed its span; the span's crc is then
+// in `crc`.  `chain` carries the crc from segment to segment of a span.
+template <int K>
+__device__ __forceinline__ bool process_seg(const Slot& s, u32x4 (&d)[K], uint32_t s0,
+                                            uint32_t lane, uint32_t& chain, uint32_t& crc) {
+  const uint32_t init = (s.flags & kSlotFirst) ? s.init : chain;
+  const uint32_t h = static_cast<uint32_t>(s.start & 15u);
+  const uint32_t hn = h + s.n;  // main region: chunks [0, hn >> 4) of a0
+  const uint64_t a0 = s.start & ~uint64_t(15);
+  uint32_t reg;  // register after the main region (or ~init if none)
+  if (hn >= 16u) {
+    const uint32_t pad = kSegChunks - (hn >> 4);
+    uint32_t r[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) r[k] = 0u;
-      if (lane == 0) r[0] = ~it_init;
-      for (uint32_t i = 0; i < cp; ++i) {
-        if (i + 1 < cp) {
-          load_group<K>(it, i + 1, lane, nxt);
-        } else if (nx_valid && nx.cp) {
-          load_group<K>(nx, 0, lane, nxt);
-        }
-        feed_chunks<K>(s0, r, cur);
-#pragma unroll
-        for (int k = 0; k < K; ++k) cur[k] = nxt[k];
-      }
-      reg = fold_wave<K>(r, cp, lane);
-    } else if (cp) {
-      // ---- general path: unaligned start, front padding, ragged end ----
-      const uint32_t inj = (it_init == 0u) ? lds_ld(kLdsHead0 + (it.h << 2))
-                                           : unshift_bytes(s0, ~it_init, it.h);
-      const uint32_t h = it.h;
+    for (int k = 0; k < K; ++k) r[k] = 0u;
+    if (hn == 4096u && h == 0u) {
+      // fast path: a whole aligned 4 KiB segment; ~init enters at lane 0,
+      // chain 0, before any byte
+      if (lane == 0) r[0] = ~init;
+      feed_chunks<K>(s0, r, d);
+    } else {
+      // general path: chunk 0 sits at virtual chunk `pad` (lane pad%64,
+      // chain pad/64): mask its first h bytes and inject ~init * x^(-8h) there
+      const uint32_t inj = (init == 0u) ? lds_ld(kLdsHead0 + (h << 2))
+                                        : unshift_bytes(s0, ~init, h);
       const uint32_t m0 = h == 0 ? ~0u : (h >= 4 ? 0u : (~0u << (8 * h)));
       const uint32_t m1 = h <= 4 ? ~0u : (h >= 8 ? 0u : (~0u << (8 * (h - 4))));
       const uint32_t m2 = h <= 8 ? ~0u : (h >= 12 ? 0u : (~0u << (8 * (h - 8))));
       const uint32_t m3 = h <= 12 ? ~0u : (~0u << (8 * (h - 12)));
-      // chunk 0 of the span sits at virtual chunk `pad`: lane l0, chain k0,
-      // group i0 (all uniform)
-      const uint32_t kcp = K * cp;
-      const uint32_t l0 = it.pad / kcp;
-      const uint32_t k0 = (it.pad - l0 * kcp) / cp;
-      const uint32_t i0 = it.pad - l0 * kcp - k0 * cp;
-      uint32_t r[K];
+      const uint32_t l0 = pad & 63u, k0 = pad >> 6;
+      u32x4 e[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) r[k] = 0u;
-
-      for (uint32_t i = 0; i < cp; ++i) {
-        // prefetch the next group (this item or the next one)
-        if (i + 1 < cp) {
-          load_group<K>(it, i + 1, lane, nxt);
-        } else if (nx_valid && nx.cp) {
-          load_group<K>(nx, 0, lane, nxt);
+      for (int k = 0; k < K; ++k) {
+        e[k] = d[k];
+        if (static_cast<uint32_t>(k) == k0 && lane == l0) {
+          e[k].x &= m0;
+          e[k].y &= m1;
+          e[k].z &= m2;
+          e[k].w &= m3;
+          r[k] = inj;
         }
-        // chunk 0 of the span: mask its leading bytes, inject the register
-        if (i == i0) {
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            if (static_cast<uint32_t>(k) == k0 && lane == l0) {
-              cur[k].x &= m0;
-              cur[k].y &= m1;
-              cur[k].z &= m2;
-              cur[k].w &= m3;
-              r[k] = inj;
-            }
-          }
-        }
-        feed_chunks<K>(s0, r, cur);
-#pragma unroll
-        for (int k = 0; k < K; ++k) cur[k] = nxt[k];
       }
-      // chains made only of virtual chunks (in front of the span) carry
-      // garbage: they must be zero
-      {
-        const int32_t qlast = static_cast<int32_t>(lane * kcp + cp - 1u) -
-                              static_cast<int32_t>(it.pad);
+      feed_chunks<K>(s0, r, e);
+      // chains of virtual chunks (in front of the span) carry garbage
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-          if (qlast + k * static_cast<int32_t>(cp) < 0) r[k] = 0u;
-      }
-      reg = fold_wave<K>(r, cp, lane);
-    } else {
-      reg = ~it_init;
-      if (nx_valid && nx.cp) load_group<K>(nx, 0, lane, cur);
+      for (int k = 0; k < K; ++k)
+        if (lane + 64u * k < pad) r[k] = 0u;
     }
+    reg = fold_wave_c2<K>(r, lane);
+  } else {
+    reg = ~init;
+  }
 
-    // ragged tail: bytes [max(e0, start), end) inside chunk [e0, e0+16)
-    const uint64_t e0 = end & ~uint64_t(15);
-    if (end > e0) {
+  // ragged tail: bytes [o, e) of the chunk at a0 + (hn & ~15)
+  const uint32_t e = hn & 15u;
+  if (e != 0u) {
+    const uint32_t o = hn < 16u ? h : 0u;
+    const uint64_t e0 = a0 + (hn & ~15u);
+    uint32_t t[4];
+#ifdef WIPDB_TAIL_ASM
+    tail_chunk(e0, t);  // the chunk holding `end` is mapped (it has span bytes)
+#else
+    {
       const uint32_t* tp = reinterpret_cast<const uint32_t*>(e0);
-      const uint32_t o = it.start > e0 ? static_cast<uint32_t>(it.start - e0) : 0u;
-      const uint32_t e = static_cast<uint32_t>(end - e0);
-      uint32_t t[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) t[j] = (4u * j < e) ? tp[j] : 0u;
-      uint32_t i = o;
-      if (o == 0) {
+    }
+#endif
+    uint32_t i = o;
+    if (o == 0) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          if (4u * j + 4u <= e) {
-            reg = feed_word(s0, reg, t[j]);
-            i += 4;
-          }
-      }
-      for (; i < e; ++i) {
-        const uint32_t wd = i < 4 ? t[0] : (i < 8 ? t[1] : (i < 12 ? t[2] : t[3]));
-        reg = feed_byte(s0, reg, (wd >> (8 * (i & 3))) & 0xffu);
-      }
+      for (int j = 0; j < 3; ++j)
+        if (4u * j + 4u <= e) {
+          reg = feed_word(s0, reg, t[j]);
+          i += 4;
+        }
     }
-    const uint32_t crc = ~reg;
-
-    if (it.rest > it.n) {
-      nx_init = crc;  // next segment of the same span continues from here
-    } else {
-      out(it.span, crc, lane);
+    for (; i < e; ++i) {
+      const uint32_t wd = i < 4 ? t[0] : (i < 8 ? t[1] : (i < 12 ? t[2] : t[3]));
+      reg = feed_byte(s0, reg, (wd >> (8 * (i & 3))) & 0xffu);
     }
-    if (!nx_valid) break;
-    it = nx;
-    it_init = nx_init;
   }
+  const uint32_t c = ~reg;
+  if (s.flags & kSlotLast) {
+    crc = c;
+    return true;
+  }
+  chain = c;
+  return false;
+}
+
+// Per-wave output buffer: lane j holds the crc of the wave's (base + j)-th
+// span; one vector store per 64 spans (flush(first_ordinal, crc_lane,
+// nvalid) is called with all lanes active).
+struct OutBuf {
+  uint32_t v = 0;      // per lane
+  uint32_t fill = 0;   // uniform: lanes filled
+  uint64_t base = 0;   // uniform: wave-local ordinal of lane 0
+};
+
+// The wave loop: a register ring of WIPDB_RING_SLOTS slots (2 or 3).  While
+// segment j is processed, the loads of the next 1 or 2 segments are in
+// flight (4-8 KiB per wave, 64-128 KiB per CU, ahead of the compute).  Every
+// step issues exactly 4 loads.
+template <int K, typename Src, typename Flush>
+__device__ __forceinline__ void run_waves(Src& src, uint64_t first_span, uint64_t span_stride,
+                                          const void* dummy, Flush flush) {
+  static_assert(K == 4, "the ring is written for 4 chunks per lane");
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t l4 = (threadIdx.x & 31u) * 4u;
+  const uint32_t s0 = l4 | ((l4 | 0x80u) << 8) | (1u << 16);
+  if (first_span >= src.count) return;
+
+  SegCursor<Src> cur;
+  cur.begin(src, first_span, span_stride, lane);
+  uint32_t chain = 0;
+  OutBuf ob;
+
+  auto finish = [&](const Slot& sl, u32x4 (&d)[4]) {
+    uint32_t crc = 0;
+    if (process_seg<K>(sl, d, s0, lane, chain, crc)) {
+#if WIPDB_OUTBUF
+      ob.v = (lane == ob.fill) ? crc : ob.v;
+      if (++ob.fill == 64u) {
+        flush(ob.base, ob.v, 64u);
+        ob.base += 64u;
+        ob.fill = 0u;
+      }
+#else
+      flush(ob.base, crc, 1u);
+      ob.base += 1u;
+#endif
+    }
+  };
+
+#if WIPDB_RING_SLOTS == 3
+  u32x4 bA[4], bB[4], bC[4];
+  Slot sA = cur.next(src, lane);
+  issue_seg(sA, lane, dummy, bA);
+  Slot sB = cur.next(src, lane);
+  issue_seg(sB, lane, dummy, bB);
+  for (;;) {
+    Slot sC = cur.next(src, lane);
+    issue_seg(sC, lane, dummy, bC);
+    if (!(sA.flags & kSlotValid)) break;
+    finish(sA, bA);
+
+    sA = cur.next(src, lane);
+    issue_seg(sA, lane, dummy, bA);
+    if (!(sB.flags & kSlotValid)) break;
+    finish(sB, bB);
+
+    sB = cur.next(src, lane);
+    issue_seg(sB, lane, dummy, bB);
+    if (!(sC.flags & kSlotValid)) break;
+    finish(sC, bC);
+  }
+#else
+  // 2-slot ping-pong: one segment's loads in flight while one is computed
+  u32x4 bA[4], bB[4];
+  Slot sA = cur.next(src, lane);
+  issue_seg(sA, lane, dummy, bA);
+  for (;;) {
+    Slot sB = cur.next(src, lane);
+    issue_seg(sB, lane, dummy, bB);
+    if (!(sA.flags & kSlotValid)) break;
+    finish(sA, bA);
+
+    sA = cur.next(src, lane);
+    issue_seg(sA, lane, dummy, bA);
+    if (!(sB.flags & kSlotValid)) break;
+    finish(sB, bB);
+  }
+#endif
+  if (ob.fill) flush(ob.base, ob.v, ob.fill);
 }
 
 // Copy the device tables into LDS: main tables replicated 32x, the rest
@@ -441,7 +564,7 @@ __device__ __forceinline__ void load_tables(uint8_t* lds, const DevTables* __res
     const uint32_t e = e4 * 4u;
     const uint32_t b = e >> 6, u = (e >> 5) & 1u;
     const uint32_t v = u ? tab->t0[b] : tab->t1[b];
-    *reinterpret_cast<u32x4*>(lds + e * 4u) = u32x4{v, v, v, v};
+    *reinterpret_cast<u32x4*>(lds + kLdsMain + e * 4u) = u32x4{v, v, v, v};
   }
   const u32x4* src = reinterpret_cast<const u32x4*>(tab->shift);
   u32x4* dst = reinterpret_cast<u32x4*>(lds + kLdsShift);
@@ -468,27 +591,31 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  DescSource src{base, offsets, lengths, inits, count, 0u, ~uint64_t(0) >> 1, 0, 0, 0};
+  DescSource src{base, offsets, lengths, inits, count, 0u, 0, 0, 0, 0, 64u};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves<kChains>(src, wave_id(), static_cast<uint64_t>(gridDim.x) * kWaves,
-                     [&](uint64_t s, uint32_t crc, uint32_t lane) {
-                       if (lane == 0) out[s] = msk ? mask_crc(crc) : crc;
-                     });
+  const uint64_t first = wave_id();
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves;
+  run_waves<kChains>(src, first, stride, tab, [&](uint64_t ord, uint32_t crc, uint32_t nvalid) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane < nvalid) out[first + (ord + lane) * stride] = msk ? mask_crc(crc) : crc;
+  });
 }
 
 // Fixed-size blocks at a fixed stride.
 __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
-    const uint8_t* __restrict__ base, uint64_t stride, uint32_t length, uint32_t init,
+    const uint8_t* __restrict__ base, uint64_t stride_bytes, uint32_t length, uint32_t init,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags,
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  StridedSource src{base, stride, length, init, count};
+  StridedSource src{base, stride_bytes, length, init, count};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves<kChains>(src, wave_id(), static_cast<uint64_t>(gridDim.x) * kWaves,
-                     [&](uint64_t s, uint32_t crc, uint32_t lane) {
-                       if (lane == 0) out[s] = msk ? mask_crc(crc) : crc;
-                     });
+  const uint64_t first = wave_id();
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves;
+  run_waves<kChains>(src, first, stride, tab, [&](uint64_t ord, uint32_t crc, uint32_t nvalid) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane < nvalid) out[first + (ord + lane) * stride] = msk ? mask_crc(crc) : crc;
+  });
 }
 
 // Read-side verify: block = base + off, n = handle size; crc over n+1 bytes
@@ -499,18 +626,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  DescSource src{base, offsets, lengths, nullptr, count, 1u, ~uint64_t(0) >> 1, 0, 0, 0};
-  run_waves<kChains>(src, wave_id(), static_cast<uint64_t>(gridDim.x) * kWaves,
-                     [&](uint64_t s, uint32_t crc, uint32_t lane) {
-                       if (lane == 0) {
-                         const uint8_t* t = base + offsets[s] + lengths[s] + 1;
-                         const uint32_t stored = uint32_t(t[0]) | (uint32_t(t[1]) << 8) |
-                                                 (uint32_t(t[2]) << 16) |
-                                                 (uint32_t(t[3]) << 24);
-                         const uint32_t rot = stored - 0xa282ead8u;
-                         status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;
-                       }
-                     });
+  DescSource src{base, offsets, lengths, nullptr, count, 1u, 0, 0, 0, 0, 64u};
+  const uint64_t first = wave_id();
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves;
+  run_waves<kChains>(src, first, stride, tab, [&](uint64_t ord, uint32_t crc, uint32_t nvalid) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane < nvalid) {
+      const uint64_t s = first + (ord + lane) * stride;
+      const uint8_t* t = base + offsets[s] + lengths[s] + 1;
+      const uint32_t stored = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) |
+                              (uint32_t(t[3]) << 24);
+      const uint32_t rot = stored - 0xa282ead8u;
+      status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;
+    }
+  });
 }
 
 // Read-stream ceiling: the same 16-byte nontemporal loads over fixed-size
