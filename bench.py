@@ -61,11 +61,6 @@ def parse():
     return p.parse_args()
 
 
-def shard(rank: int, world: int, blocks_per_rank: int):
-    """Weak scaling: rank r owns global blocks [r*B, (r+1)*B)."""
-    return rank * blocks_per_rank, blocks_per_rank
-
-
 def cpu_baseline(seed, blocks_on_gpu_crc, first_block, target_s):
     """Reference kv::crc32c on this host over a bounded sample of rank 0's
     blocks (regenerated from the seed), 1 thread; plus the parity check of
@@ -142,6 +137,7 @@ def main():
     import torch
     import torch.distributed as dist
     from wipdb_amd import Engine
+    from wipdb_amd.shard import block_shard, max_over_ranks
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -154,7 +150,7 @@ def main():
     torch.cuda.set_device(dev)
 
     eng = Engine(local)
-    first, nblk = shard(rank, world, a.blocks)
+    first, nblk = block_shard(rank, world, a.blocks)  # weak scaling, no collective
     data = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     eng.fill_splitmix64_device(data, SEED, first_word=first * BLOCK // 8, stream=stream.cuda_stream)
@@ -189,12 +185,8 @@ def main():
     kern_ms = sorted(s.elapsed_time(e) for s, e in ev)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    kmax = torch.tensor([kern_avg_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kmax, op=dist.ReduceOp.MAX)
-    elapsed_max = float(tmax.item())
+    elapsed_max = max_over_ranks(elapsed, dev)
+    kern_avg_ms = max_over_ranks(kern_avg_ms, dev)
 
     rs = None
     if a.readstream:
