@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Secondary measurements (BASELINE.json configs 3 and 5, and the
+PCIe-inclusive host path) -- one JSON line each, for DESIGN.md.
+
+  mixed      config 3: Zipf(0.99) sizes over {512 .. 64 Ki} (+0..L/8 jitter),
+             SST-packed at unaligned offsets (prev + L + 5), device-resident:
+             per-bucket GiB/s, the mixed batch's GiB/s, and p50/p99 latency of
+             SST-sized batches (one ~2 MiB SST per launch, synchronised).
+  sst        config 5: 8Binsert-shaped SSTs (~500 data blocks of 4097..4225
+             bytes incl. the type byte, one ~18 KiB index block, one ~25 KiB
+             filter block, one metaindex block) in HOST memory, checksummed
+             through hcrc_batch(HOST_PTRS): pinned staging + H2D + kernel +
+             D2H, overlapped -- the PCIe-inclusive end-to-end rate.
+  host4k     the headline 1 M x 4 KiB blocks from host memory (PCIe-inclusive).
+
+Every batch is checked against the library's host CPU path on a sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from wipdb_amd import Engine, cpu_batch  # noqa: E402
+
+BUCKETS = [512, 1024, 2048, 4096, 8192, 16384, 32768, 65536]
+
+
+def zipf_spans(rng, nbytes, buckets, theta=0.99, start=3):
+    p = 1.0 / np.arange(1, len(buckets) + 1) ** theta
+    p /= p.sum()
+    est = int(nbytes / (np.dot(p, buckets) * 1.07 + 5)) + 16
+    L = np.asarray(buckets)[rng.choice(len(buckets), est, p=p)]
+    n = L + rng.integers(0, L // 8 + 1)
+    offs = start + np.concatenate([[0], np.cumsum(n + 5)[:-1]])
+    keep = offs + n <= nbytes
+    return offs[keep].astype(np.uint64), n[keep].astype(np.uint32), L[keep]
+
+
+def dev(a, d):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).to(d)
+
+
+def time_kernel(fn, stream, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(reps):
+        fn()
+    e.record(stream)
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps / 1e3
+
+
+def check_sample(host, offs, lens, got, rng, k=4000):
+    idx = rng.choice(offs.size, min(k, offs.size), replace=False)
+    want = cpu_batch(host, offs[idx], lens[idx])
+    return int((want != got[idx]).sum())
+
+
+def run_mixed(eng, d, stream, rng, gib):
+    nbytes = int(gib * 2**30)
+    host = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).to(d)
+    res = {"config": "3 mixed (Zipf 0.99, SST-packed, unaligned)", "buckets": {}}
+    offs, lens, L = zipf_spans(rng, nbytes, BUCKETS)
+    do, dl = dev(offs, d), dev(lens, d)
+    out = torch.empty(offs.size, dtype=torch.int32, device=d)
+    t = time_kernel(lambda: eng.batch_device(dbuf, do, dl, None, out, stream=stream.cuda_stream),
+                    stream, 10)
+    got = out.cpu().numpy().view(np.uint32)
+    res["mixed"] = {"spans": int(offs.size), "bytes": int(lens.sum()),
+                    "GiBps": round(float(lens.sum()) / t / 2**30, 1),
+                    "mismatches_in_sample": check_sample(host, offs, lens, got, rng)}
+    for b in BUCKETS:  # one batch per bucket: same packing, only this size
+        ob, lb, _ = zipf_spans(rng, nbytes, [b])
+        dob, dlb = dev(ob, d), dev(lb, d)
+        outb = torch.empty(ob.size, dtype=torch.int32, device=d)
+        tb = time_kernel(lambda: eng.batch_device(dbuf, dob, dlb, None, outb,
+                                                  stream=stream.cuda_stream), stream, 10)
+        gotb = outb.cpu().numpy().view(np.uint32)
+        res["buckets"][str(b)] = {"spans": int(ob.size),
+                                  "GiBps": round(float(lb.sum()) / tb / 2**30, 1),
+                                  "mismatches_in_sample": check_sample(host, ob, lb, gotb, rng,
+                                                                       1000)}
+    # latency of SST-sized batches: ~2 MiB of the mixed spans per launch
+    cum = np.cumsum(lens.astype(np.int64) + 5)
+    per = int(np.searchsorted(cum, 2 << 20))
+    lat = []
+    outs = torch.empty(per, dtype=torch.int32, device=d)
+    for i in range(300):
+        lo = (i * per) % max(1, offs.size - per)
+        o_i, l_i = do[lo:lo + per], dl[lo:lo + per]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    lat = np.array(lat[20:]) * 1e6
+    res["sst_batch_latency_us"] = {"spans_per_batch": per, "p50": round(float(np.percentile(lat, 50)), 1),
+                                   "p99": round(float(np.percentile(lat, 99)), 1)}
+    del dbuf
+    return res
+
+
+def sst_layout(rng, n_sst):
+    """8Binsert-shaped SSTs (test_bench/8Binsert.sh): spans cover contents +
+    type byte; every block is followed by its 4-byte crc slot."""
+    offs, lens, cur = [], [], 0
+    for _ in range(n_sst):
+        for _ in range(int(rng.integers(480, 520))):   # data blocks
+            n = int(rng.integers(4096, 4225)) + 1
+            offs.append(cur)
+            lens.append(n)
+            cur += n + 4
+        for n in (int(rng.integers(15000, 20000)), int(rng.integers(24000, 26000)),
+                  int(rng.integers(40, 100))):          # index, filter, metaindex
+            offs.append(cur)
+            lens.append(n + 1)
+            cur += n + 5
+        cur += 48  # footer
+    return np.array(offs, np.uint64), np.array(lens, np.uint32), cur
+
+
+def run_sst(eng, rng, n_sst):
+    offs, lens, nbytes = sst_layout(rng, n_sst)
+    host = rng.integers(32, 127, nbytes, dtype=np.uint8)  # printable, like CompressibleString
+    eng.batch(host, offs[:1000], lens[:1000])  # warm: staging allocated
+    t0 = time.perf_counter()
+    got = eng.batch(host, offs, lens, mask_output=True)
+    t = time.perf_counter() - t0
+    idx = rng.choice(offs.size, 4000, replace=False)
+    want = cpu_batch(host, offs[idx], lens[idx], mask_output=True)
+    tc0 = time.perf_counter()
+    cpu_batch(host, offs, lens, mask_output=True, threads=16)
+    tc = time.perf_counter() - tc0
+    return {"config": "5 8Binsert SST stream, host memory, PCIe-inclusive (hcrc_batch HOST_PTRS)",
+            "ssts": n_sst, "spans": int(offs.size), "bytes": int(lens.sum()),
+            "GiBps_end_to_end": round(float(lens.sum()) / t / 2**30, 2),
+            "cpu_16_threads_GiBps": round(float(lens.sum()) / tc / 2**30, 2),
+            "mismatches_in_sample": int((want != got[idx]).sum())}
+
+
+def run_host4k(eng, rng, nblk):
+    host = rng.integers(0, 256, nblk * 4096, dtype=np.uint8)
+    offs = np.arange(nblk, dtype=np.uint64) * 4096
+    lens = np.full(nblk, 4096, np.uint32)
+    eng.batch(host, offs[:1000], lens[:1000])
+    t0 = time.perf_counter()
+    got = eng.batch(host, offs, lens)
+    t = time.perf_counter() - t0
+    idx = rng.choice(nblk, 4000, replace=False)
+    return {"config": "headline blocks from host memory (PCIe-inclusive, pageable source)",
+            "blocks": nblk, "GiBps_end_to_end": round(nblk * 4096 / t / 2**30, 2),
+            "mismatches_in_sample": int((cpu_batch(host, offs[idx], lens[idx]) != got[idx]).sum())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="mixed,sst,host4k")
+    ap.add_argument("--mixed-gib", type=float, default=2.0)
+    ap.add_argument("--ssts", type=int, default=256)
+    ap.add_argument("--host-blocks", type=int, default=1 << 18)
+    a = ap.parse_args()
+    rng = np.random.default_rng(42)
+    d = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(d)
+    with Engine(0) as eng:
+        for w in a.what.split(","):
+            if w == "mixed":
+                r = run_mixed(eng, d, stream, rng, a.mixed_gib)
+            elif w == "sst":
+                r = run_sst(eng, rng, a.ssts)
+            elif w == "host4k":
+                r = run_host4k(eng, rng, a.host_blocks)
+            else:
+                raise SystemExit(f"unknown {w}")
+            print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
