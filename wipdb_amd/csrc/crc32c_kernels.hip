@@ -7,47 +7,48 @@
 // (kv/src/table/format.cc:91-93) do one block at a time.
 //
 // Design (DESIGN.md "Kernels"):
-//   * one span per wavefront, cut into 4 KiB segments of its 16-byte chunk
-//     grid.  A segment's 256 chunks are 64*K one-chunk stripes ("virtual
-//     lanes"): lane l runs K = 4 independent CRC chains over chunks l,
-//     64+l, 128+l, 192+l, so each 16-byte load instruction of the wave reads
-//     one contiguous KiB (fully coalesced).  The K chains give the
-//     LDS-latency-bound byte scan instruction-level parallelism.
+//   * a wave CRCs kGroups = 2 spans at once: lanes 0-31 one span, lanes
+//     32-63 another, each group walking its own stream of spans.  A span is
+//     cut into 4 KiB segments of its 16-byte chunk grid.  In a segment,
+//     lane l of a group runs kChains = 8 independent CRC chains over chunks
+//     l, 32+l, ..., 224+l, so each 16-byte load instruction of the wave
+//     reads two contiguous 512 B runs (fully coalesced), and the 8 chains
+//     give the LDS-latency-bound scan instruction-level parallelism.
 //   * CRC arithmetic is table-driven from LDS (CDNA4 has no carry-less
 //     multiply and this is a byte scan, not a contraction: no MFMA):
-//     slicing-by-2 tables replicated 32x so lane l always reads bank l&31 --
-//     every lookup is bank-conflict free -- and each lookup address is built
-//     by ONE v_perm_b32 (table byte | lane byte | region byte).
-//   * the 256 stripe registers are folded by a GF(2) tree: an in-lane Horner
-//     step over the 4 chains (shift by 1 KiB), then a 6-level wavefront
-//     butterfly (DPP row shifts, then v_readlane),
+//     slicing-by-4 tables replicated 32x so lane l always reads bank l&31 --
+//     every lookup is bank-conflict free -- and each lookup address is ONE
+//     v_perm_b32 (table bits | data byte | lane byte); 160 KiB of LDS.
+//   * the 256 stripe registers of a group fold by a GF(2) tree: an in-lane
+//     Horner step over the 8 chains (shift by 512 B), then a 5-level
+//     butterfly over the group's lanes (DPP row shifts, then v_readlane),
 //        reg(v) = shift(reg(v), 16 * 2^t bytes) ^ reg(v + 2^t),
 //     where shift by 16*2^j bytes is 4 lookups in a "multiply by
 //     x^(8*16*2^j) mod P" table (the carry-less combine of the reference's
-//     CombineCRC, crc32c.cc:640-657, done with tables).
+//     CombineCRC, crc32c.cc:640-657, done with tables).  Both groups fold in
+//     the same instructions, so the fold costs half as much per span.
 //   * unaligned starts: the first chunk's leading bytes are zeroed and the
 //     register injected there is pre-un-shifted (~init * x^(-8h)) so it
 //     equals ~init at the first real byte; the ragged end (< 16 bytes) is
 //     fed after the fold.  Segments of one span are chained through init.
 //     So any offset/length/init is bit-exact.
 //   * latency hiding: persistent grid (1 workgroup of 16 waves per CU), each
-//     wave walks its spans' segments through a 3-slot register ring (two
-//     segments of loads in flight while one is computed); 64 span
-//     descriptors are fetched per vector load.
+//     wave walks its segment pairs through a register ring (the next
+//     segments' loads are in flight while one is computed); 32 span
+//     descriptors per group are fetched per vector load.
+//   * the wave loop keeps segment geometry in 32-bit offsets and counts
+//     spans down: uniform 64-bit compares become VALU compares moved to SCC,
+//     which hipcc 7.2 mis-scheduled in this loop.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "crc32c_device.h"
 
-#ifndef WIPDB_FOLD_SELECT
-#define WIPDB_FOLD_SELECT 0
+#ifndef WIPDB_EARLY_REISSUE
+#define WIPDB_EARLY_REISSUE 0
 #endif
-#ifndef WIPDB_OUTBUF
-#define WIPDB_OUTBUF 1
-#endif
-#ifndef WIPDB_RING_SLOTS
-#define WIPDB_RING_SLOTS 3
-#endif
+
+
 
 namespace wipdb {
 namespace dev {
@@ -56,6 +57,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
 typedef __attribute__((address_space(3))) const uint32_t l_u32;
 
+constexpr int G = kGroupLanes;  // lanes per group (32)
+constexpr int K = kChains;      // chains per lane (8)
+constexpr int S = kGroups;      // groups (spans) per wave (2)
+static_assert(G * K == 256 && S * G == 64, "a group segment is 256 chunks");
+
 // ---------------------------------------------------------------------------
 // LDS helpers (dynamic LDS starts at address 0: no static __shared__ here)
 // ---------------------------------------------------------------------------
@@ -63,45 +69,59 @@ __device__ __forceinline__ uint32_t lds_ld(uint32_t addr) {
   return *reinterpret_cast<l_u32*>(static_cast<uintptr_t>(addr));
 }
 
-// s0 = lane constant: byte0 = (lane&31)*4 (T1), byte1 = (lane&31)*4|0x80
-// (T0), byte2 = 0x01 (the 64 KiB region of the main tables).
-constexpr uint32_t kSelT1B0 = 0x0c060004u;  // [s0.b0, x.b0, s0.b2, 0] -> T1[x.b0]
-constexpr uint32_t kSelT0B1 = 0x0c060105u;  // [s0.b1, x.b1, s0.b2, 0] -> T0[x.b1]
+// s0 = lane constant: byte0 = (lane&31)*4, byte1 = (lane&31)*4 | 0x80,
+// byte2 = 0x00, byte3 = 0x01.  Table t's entry for data byte p of x is at
+// kLdsMain + perm(s0, x, sel(t, p)):
+//   [s0.b(t&1), x.b(p), s0.b(2 + (t>>1)), 0].
+__host__ __device__ constexpr uint32_t sel_tab(uint32_t t, uint32_t p) {
+  return 0x0c000000u | ((6u + (t >> 1)) << 16) | (p << 8) | (4u + (t & 1u));
+}
 
-// Feed one little-endian 32-bit word into register r (slicing-by-2 twice).
+template <uint32_t T, uint32_t P>
+__device__ __forceinline__ uint32_t look(uint32_t s0, uint32_t x) {
+  return lds_ld(kLdsMain + __builtin_amdgcn_perm(s0, x, sel_tab(T, P)));
+}
+
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// One slicing-by-4 word step in "x form": x = register ^ word; returns the
+// register after the word's 4 bytes XOR the next word (0 at a chain end):
+// 4 v_perm_b32 + 4 ds_read_b32 + 2 v_bitop3_b32.
+__device__ __forceinline__ uint32_t step4(uint32_t s0, uint32_t x, uint32_t w_next) {
+  return xor3(xor3(look<3, 0>(s0, x), look<2, 1>(s0, x), look<1, 2>(s0, x)), look<0, 3>(s0, x),
+              w_next);
+}
+
 __device__ __forceinline__ uint32_t feed_word(uint32_t s0, uint32_t r, uint32_t w) {
-  const uint32_t x = r ^ w;
-  const uint32_t y = lds_ld(__builtin_amdgcn_perm(s0, x, kSelT1B0)) ^
-                     lds_ld(__builtin_amdgcn_perm(s0, x, kSelT0B1)) ^ (x >> 16);
-  return lds_ld(__builtin_amdgcn_perm(s0, y, kSelT1B0)) ^
-         lds_ld(__builtin_amdgcn_perm(s0, y, kSelT0B1)) ^ (y >> 16);
+  return step4(s0, r ^ w, 0u);
 }
 
-// One word step in "x form": x = register ^ word; returns the register after
-// the word's 4 bytes XOR the next word (w_next = 0 at the end of a chain).
-// Written so the compiler forms v_xor_b32_sdwa + v_xor3_b32 (8 VALU/word).
-__device__ __forceinline__ uint32_t step_x(uint32_t s0, uint32_t x, uint32_t w_next) {
-  const uint32_t y = lds_ld(__builtin_amdgcn_perm(s0, x, kSelT1B0)) ^
-                     lds_ld(__builtin_amdgcn_perm(s0, x, kSelT0B1)) ^ (x >> 16);
-  const uint32_t yw = (y >> 16) ^ w_next;
-  return lds_ld(__builtin_amdgcn_perm(s0, y, kSelT1B0)) ^
-         lds_ld(__builtin_amdgcn_perm(s0, y, kSelT0B1)) ^ yw;
-}
-
-// Feed one 16-byte chunk into K independent chains (interleaved word by word).
-template <int K>
+// Feed one 16-byte chunk into each of the K chains (interleaved by word).
+// Feed one 16-byte chunk into each of chains [K0, K1) (interleaved by word,
+// so their lookups are in flight together).
+template <int K0, int K1>
 __device__ __forceinline__ void feed_chunks(uint32_t s0, uint32_t (&r)[K], const u32x4 (&d)[K]) {
-  uint32_t x[K];
+  constexpr int I = K1 - K0;
+  uint32_t x[I];
 #pragma unroll
-  for (int k = 0; k < K; ++k) x[k] = r[k] ^ d[k].x;
+  for (int i = 0; i < I; ++i) x[i] = r[K0 + i] ^ d[K0 + i].x;
 #pragma unroll
-  for (int k = 0; k < K; ++k) x[k] = step_x(s0, x[k], d[k].y);
+  for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[K0 + i].y);
 #pragma unroll
-  for (int k = 0; k < K; ++k) x[k] = step_x(s0, x[k], d[k].z);
+  for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[K0 + i].z);
 #pragma unroll
-  for (int k = 0; k < K; ++k) x[k] = step_x(s0, x[k], d[k].w);
+  for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[K0 + i].w);
 #pragma unroll
-  for (int k = 0; k < K; ++k) r[k] = step_x(s0, x[k], 0u);
+  for (int i = 0; i < I; ++i) r[K0 + i] = step4(s0, x[i], 0u);
+}
+
+// Feed one byte (Sarwate step with this lane's T0 replica).
+__device__ __forceinline__ uint32_t feed_byte(uint32_t s0, uint32_t r, uint32_t b) {
+  const uint32_t x = (r ^ b) & 0xffu;
+  return lds_ld(kLdsMain + ((x << 8) | (s0 & 0xffu))) ^ (r >> 8);
 }
 
 // DPP row shift-left: lane l receives lane l+n of its 16-lane row (0 past
@@ -112,30 +132,23 @@ __device__ __forceinline__ uint32_t row_shl(uint32_t v) {
       __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x100 | N, 0xF, 0xF, true));
 }
 
-// Feed one byte (Sarwate step with this lane's T0 replica).
-__device__ __forceinline__ uint32_t feed_byte(uint32_t s0, uint32_t r, uint32_t b) {
-  const uint32_t x = (r ^ b) & 0xffu;
-  return lds_ld(kLdsMain + ((x << 8) | ((s0 >> 8) & 0xffu))) ^ (r >> 8);
-}
-
-// r * x^(8 * 16 * 2^J) mod P: 4 lookups in shift table J.  The table base
-// is a compile-time constant that lands in the ds_read offset field, so
+// r * x^(8 * 16 * 2^J) mod P, XOR p: 4 lookups in shift table J.  The table
+// base is a compile-time constant that lands in the ds_read offset field, so
 // each address is one v_lshlrev_b32_sdwa (byte select).
 template <uint32_t J>
-__device__ __forceinline__ uint32_t shift_pow2_c(uint32_t r) {
+__device__ __forceinline__ uint32_t shift_xor(uint32_t r, uint32_t p) {
   constexpr uint32_t base = kLdsShift + J * 4096u;
-  static_assert(base + 4096u <= 65536u, "ds_read offset field is 16 bits");
-  return lds_ld(base + ((r & 0xffu) << 2)) ^
-         lds_ld(base + 1024u + (((r >> 8) & 0xffu) << 2)) ^
-         lds_ld(base + 2048u + (((r >> 16) & 0xffu) << 2)) ^
-         lds_ld(base + 3072u + ((r >> 24) << 2));
+  static_assert(J < kNumShift && base + 4096u <= 65536u, "ds_read offset field is 16 bits");
+  return xor3(xor3(lds_ld(base + ((r & 0xffu) << 2)), lds_ld(base + 1024u + (((r >> 8) & 0xffu) << 2)),
+                   lds_ld(base + 2048u + (((r >> 16) & 0xffu) << 2))),
+              lds_ld(base + 3072u + ((r >> 24) << 2)), p);
 }
 
-// Un-feed h zero bytes (register that becomes r after h zero bytes).
+// Un-feed h zero bytes (the register that becomes r after h zero bytes).
 __device__ __forceinline__ uint32_t unshift_bytes(uint32_t s0, uint32_t r, uint32_t h) {
   for (uint32_t i = 0; i < h; ++i) {
     const uint32_t idx = lds_ld(kLdsInvTop + ((r >> 24) << 2));
-    const uint32_t t0 = lds_ld(kLdsMain + ((idx << 8) | ((s0 >> 8) & 0xffu)));
+    const uint32_t t0 = lds_ld(kLdsMain + ((idx << 8) | (s0 & 0xffu)));
     r = ((r ^ t0) << 8) | idx;
   }
   return r;
@@ -152,78 +165,27 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) {
 // ---------------------------------------------------------------------------
 // Segments.  A span is cut at 4 KiB boundaries of its 16-byte chunk grid:
 // segment = [start, start+n) with n = min(rest, 4096 - (start & 15)), so its
-// main region [start&~15, end&~15) holds at most 256 chunks = one chunk per
-// chain (64 lanes x K=4).  Every fold therefore uses the compile-time tables
-// of fold_wave_c2, and every segment is one load group.  Segments of one
-// span are chained: init of segment k+1 = crc of segment k (Extend).
-// All fields are wave-uniform.
+// main region holds at most 256 chunks = one chunk per chain of its group.
+// Geometry is kept in 32-bit offsets from the 16-byte aligned base:
+// hn = (start & 15) + n; the main region is chunks [0, hn >> 4), the ragged
+// tail hn & 15 bytes after it.  All fields are uniform.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSegChunks = 64u * kChains;  // 256 chunks = 4 KiB
+constexpr uint32_t kSegChunks = 256;
 constexpr uint32_t kSlotFirst = 1u, kSlotLast = 2u, kSlotValid = 4u;
 
-// Segment geometry is kept in 32-bit offsets from the segment's 16-byte
-// aligned base: hn = h + n where h = start & 15.  The main region is
-// chunks [0, hn >> 4) of the base, the ragged tail is hn & 15 bytes after it.
-// (Uniform 64-bit compares are VALU compares whose result must be moved to
-// SCC; hipcc 7.2 mis-schedules that pattern next to another such compare, so
-// the wave loop avoids them.)
 struct Slot {
+  uint64_t span;   // span index (output slot)
   uint64_t start;  // first byte (absolute address)
   uint32_t n;      // bytes in this segment
   uint32_t init;   // span init (first segment only)
   uint32_t flags;  // kSlotFirst | kSlotLast | kSlotValid
 };
 
-// Issues this lane's K = 4 chunk loads of segment s.  Virtual chunk
-// v = 64*k + lane (chain k of this lane) holds chunk q = v - pad of the main
-// region, so load k of the wave reads 64 consecutive chunks: one contiguous
-// KiB per instruction, fully coalesced.  Virtual chunks in front (q < 0)
-// read chunk 0 instead (always mapped: it holds the span's first byte); the
-// chains they feed are overwritten by the injection or zeroed before the
-// fold, so their data never matters.  Slots without a main region (or
-// invalid slots) load the KiB at `dummy` so that EVERY slot issues exactly
-// 4 vector loads: the ring stays regular.
-//
-// The issue is branch-free so hipcc's waitcnt pass sees the same 4 loads
-// per slot on every path and can leave the ring's other slots in flight.
-__device__ __forceinline__ void issue_seg(const Slot& s, uint32_t lane, const void* dummy,
-                                          u32x4 (&d)[4]) {
-  const uint32_t hn = static_cast<uint32_t>(s.start & 15u) + s.n;
-  const bool live = (s.flags & kSlotValid) && hn >= 16u;
-  const uint32_t pad = live ? kSegChunks - (hn >> 4) : 0u;
-  const uint64_t base = live ? (s.start & ~uint64_t(15)) : reinterpret_cast<uint64_t>(dummy);
-  const uint32_t step = live ? 64u : 0u;
-  // chunk q_k = max(64k + lane - pad, 0), branch-free
-  const uint32_t v0 = lane, v1 = lane + step, v2 = lane + 2u * step, v3 = lane + 3u * step;
-  const uint32_t q0 = v0 > pad ? v0 - pad : 0u;
-  const uint32_t q1 = v1 > pad ? v1 - pad : 0u;
-  const uint32_t q2 = v2 > pad ? v2 - pad : 0u;
-  const uint32_t q3 = v3 > pad ? v3 - pad : 0u;
-  g_u32x4* g = reinterpret_cast<g_u32x4*>(base);
-  d[0] = __builtin_nontemporal_load(g + q0);
-  d[1] = __builtin_nontemporal_load(g + q1);
-  d[2] = __builtin_nontemporal_load(g + q2);
-  d[3] = __builtin_nontemporal_load(g + q3);
-}
-
-// The 16 bytes at a 16-byte aligned address `p` (uniform) through the
-// scalar cache: the ragged tail of a segment.  The wait is inside the asm,
-// so the vector-memory counter -- and the load ring -- is never drained.
-__device__ __forceinline__ void tail_chunk(uint64_t p, uint32_t (&t)[4]) {
-  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
-  u32x4s v;
-  // early-clobber: the destination must not overlap the address registers
-  asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(v) : "s"(p) : "memory");
-  t[0] = v.x;
-  t[1] = v.y;
-  t[2] = v.z;
-  t[3] = v.w;
-}
-
 // ---------------------------------------------------------------------------
-// Span sources: where item descriptors come from.  Descriptors are fetched
-// 64 at a time by one vector load (lane j holds the wave's j-th next span)
-// and broadcast with v_readlane, so they never sit on the LDS counter.
+// Span sources: where span descriptors come from.  Group g of wave w owns
+// spans first_g, first_g + stride, ...  Descriptors are fetched G at a time
+// by one vector load (lane g*G + j holds group g's j-th next span) and
+// broadcast with v_readlane, so they never sit on the LDS counter.
 // ---------------------------------------------------------------------------
 struct DescSource {
   const uint8_t* base;
@@ -232,41 +194,40 @@ struct DescSource {
   const uint32_t* inits;
   uint64_t count;
   uint32_t extra;  // bytes added to every length (verify: +1 type byte)
-  uint64_t cache_first;
-  uint64_t c_off;
+  uint64_t c_off;  // per lane
   uint32_t c_len, c_init;
+  uint32_t cj[S];  // next cache index per group (uniform)
 
-  __device__ __forceinline__ void fetch(uint64_t first, uint64_t stride, uint32_t lane) {
-    cache_first = first;
-    const uint64_t s = first + lane * stride;
+  __device__ __forceinline__ void reset() {
     c_off = 0;
     c_len = 0;
     c_init = 0;
-    if (s < count) {
+#pragma unroll
+    for (int g = 0; g < S; ++g) cj[g] = G;
+  }
+  __device__ __forceinline__ void fetch(int g, uint64_t first, uint64_t stride, uint32_t lane) {
+    const uint64_t s = first + (lane & (G - 1)) * stride;
+    if ((lane / G) == static_cast<uint32_t>(g) && s < count) {
       c_off = __builtin_nontemporal_load(offsets + s);
       c_len = __builtin_nontemporal_load(lengths + s) + extra;
       c_init = inits ? __builtin_nontemporal_load(inits + s) : 0u;
     }
   }
-  __device__ __forceinline__ void get(uint32_t j, uint64_t& start, uint32_t& len,
-                                      uint32_t& init) const {
+  // Descriptor of span s, group g's next span (spans are visited in order,
+  // `stride` apart): the cache index advances by one, no division.
+  __device__ __forceinline__ void desc(int g, uint64_t s, uint64_t stride, uint32_t lane,
+                                       uint64_t& start, uint32_t& len, uint32_t& init) {
+    if (cj[g] >= static_cast<uint32_t>(G)) {
+      fetch(g, s, stride, lane);
+      cj[g] = 0u;
+    }
+    const uint32_t j = g * G + cj[g];
     const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c_off), j);
     const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(c_off >> 32), j);
     start = reinterpret_cast<uint64_t>(base) + ((static_cast<uint64_t>(hi) << 32) | lo);
     len = __builtin_amdgcn_readlane(c_len, j);
     init = __builtin_amdgcn_readlane(c_init, j);
-  }
-  // Descriptor of span s, the wave's next span (spans are visited in order,
-  // `stride` apart): the cache index advances by one, no division.
-  uint32_t cj;
-  __device__ __forceinline__ void desc(uint64_t s, uint64_t stride, uint32_t lane,
-                                       uint64_t& start, uint32_t& len, uint32_t& init) {
-    if (cj >= 64u) {
-      fetch(s, stride, lane);
-      cj = 0u;
-    }
-    get(cj, start, len, init);
-    ++cj;
+    ++cj[g];
   }
 };
 
@@ -276,7 +237,8 @@ struct StridedSource {
   uint32_t length;
   uint32_t init;
   uint64_t count;
-  __device__ __forceinline__ void desc(uint64_t s, uint64_t, uint32_t, uint64_t& start,
+  __device__ __forceinline__ void reset() {}
+  __device__ __forceinline__ void desc(int, uint64_t s, uint64_t, uint32_t, uint64_t& start,
                                        uint32_t& len, uint32_t& ini) const {
     start = reinterpret_cast<uint64_t>(base) + s * stride_bytes;
     len = length;
@@ -284,81 +246,34 @@ struct StridedSource {
   }
 };
 
-// ---------------------------------------------------------------------------
-// The wave loop.  out(span, crc, lane) is called once per span with the
-// finished crc (uniform).
-// ---------------------------------------------------------------------------
-// Fold the 64*K one-chunk stripe registers of a wave into the segment
-// register (uniform).  r[k] of lane l covers chunk 64k + l, i.e. sits
-// (3-k)*1 KiB + (63-l)*16 bytes before the segment end.  In-lane Horner over
-// k first (shift by 1 KiB), then the wavefront butterfly over lanes: DPP row
-// shifts for partners 1..8 lanes away, v_readlane for 16 and 32.  All table
-// indices are compile-time constants (shift by 16*2^J bytes).
-template <int K>
-__device__ __forceinline__ uint32_t fold_wave_c2(uint32_t (&r)[K], uint32_t lane) {
-  static_assert(K == 4, "the fold is written for 4 chains per lane");
-  uint32_t v = shift_pow2_c<6>(r[0]) ^ r[1];
-  v = shift_pow2_c<6>(v) ^ r[2];
-  v = shift_pow2_c<6>(v) ^ r[3];
-#if WIPDB_FOLD_SELECT
-  // every lane computes every level (no exec-mask regions); the partner
-  // value is only kept where the level applies
-  uint32_t p = row_shl<1>(v);
-  uint32_t t = shift_pow2_c<0>(v) ^ p;
-  v = (lane & 1u) == 0u ? t : v;
-  p = row_shl<2>(v);
-  t = shift_pow2_c<1>(v) ^ p;
-  v = (lane & 3u) == 0u ? t : v;
-  p = row_shl<4>(v);
-  t = shift_pow2_c<2>(v) ^ p;
-  v = (lane & 7u) == 0u ? t : v;
-  p = row_shl<8>(v);
-  t = shift_pow2_c<3>(v) ^ p;
-  v = (lane & 15u) == 0u ? t : v;
-  const uint32_t g16 = __builtin_amdgcn_readlane(v, 16);
-  const uint32_t g48 = __builtin_amdgcn_readlane(v, 48);
-  t = shift_pow2_c<4>(v) ^ (lane ? g48 : g16);
-  v = (lane & 31u) == 0u ? t : v;
-#else
-  uint32_t p = row_shl<1>(v);
-  if ((lane & 1u) == 0u) v = shift_pow2_c<0>(v) ^ p;
-  p = row_shl<2>(v);
-  if ((lane & 3u) == 0u) v = shift_pow2_c<1>(v) ^ p;
-  p = row_shl<4>(v);
-  if ((lane & 7u) == 0u) v = shift_pow2_c<2>(v) ^ p;
-  p = row_shl<8>(v);
-  if ((lane & 15u) == 0u) v = shift_pow2_c<3>(v) ^ p;
-  const uint32_t g16 = __builtin_amdgcn_readlane(v, 16);
-  const uint32_t g48 = __builtin_amdgcn_readlane(v, 48);
-  if ((lane & 31u) == 0u) v = shift_pow2_c<4>(v) ^ (lane ? g48 : g16);
-#endif
-  const uint32_t g0 = __builtin_amdgcn_readlane(v, 0);
-  const uint32_t g32 = __builtin_amdgcn_readlane(v, 32);
-  return uni(shift_pow2_c<5>(g0) ^ g32);
-}
-
-// Walks the wave's spans (first_span, first_span + stride, ...) and emits
-// their segments in order -- the load side of the pipeline.
+// Walks one group's spans (first, first + stride, ...) and emits their
+// segments in order -- the load side of the pipeline.
 template <typename Src>
 struct SegCursor {
   uint64_t span, start, stride;
-  uint32_t rest, init, first, left;  // left: spans not yet started, incl. this one
+  uint32_t rest, init, first, left;  // left: spans not yet finished, incl. this one
 
-  __device__ __forceinline__ void begin(Src& src, uint64_t s, uint64_t str, uint32_t lane) {
+  __device__ __forceinline__ void begin(Src& src, int g, uint64_t s, uint64_t str,
+                                       uint32_t lane) {
     stride = str;
     span = s;
-    left = static_cast<uint32_t>((src.count - s + str - 1) / str);  // s < count
+    // s < str always, so this is ceil((count - s) / str) or 0 -- no compare
+    left = static_cast<uint32_t>((src.count + str - 1 - s) / str);
     first = 1u;
-    src.desc(s, stride, lane, start, rest, init);
+    start = 0;
+    rest = 0;
+    init = 0;
+    if (left != 0u) src.desc(g, s, stride, lane, start, rest, init);
   }
-  __device__ __forceinline__ Slot next(Src& src, uint32_t lane) {
-    // every field defined on every path: an undef field read by issue_seg
-    // lets LLVM substitute another slot's value at the ring's merge points
-    Slot sl{0, 0, 0, 0};
+  __device__ __forceinline__ Slot next(Src& src, int g, uint32_t lane) {
+    // every field defined on every path (undef fields let LLVM substitute
+    // another slot's value at the ring's merge points)
+    Slot sl{0, 0, 0, 0, 0};
     if (left == 0u) return sl;
     const uint32_t room = 4096u - static_cast<uint32_t>(start & 15u);
     const bool last = rest <= room;
     const uint32_t n = last ? rest : room;
+    sl.span = span;
     sl.start = start;
     sl.n = n;
     sl.init = init;
@@ -367,7 +282,7 @@ struct SegCursor {
       span += stride;
       first = 1u;
       --left;
-      if (left != 0u) src.desc(span, stride, lane, start, rest, init);
+      if (left != 0u) src.desc(g, span, stride, lane, start, rest, init);
     } else {
       start += n;
       rest -= n;
@@ -377,182 +292,297 @@ struct SegCursor {
   }
 };
 
-// Processes one segment whose chunks are in d (already waited for).
-// Returns true when the segment completed its span; the span's crc is then
-// in `crc`.  `chain` carries the crc from segment to segment of a span.
-template <int K>
-__device__ __forceinline__ bool process_seg(const Slot& s, u32x4 (&d)[K], uint32_t s0,
-                                            uint32_t lane, uint32_t& chain, uint32_t& crc) {
-  const uint32_t init = (s.flags & kSlotFirst) ? s.init : chain;
-  const uint32_t h = static_cast<uint32_t>(s.start & 15u);
-  const uint32_t hn = h + s.n;  // main region: chunks [0, hn >> 4) of a0
-  const uint64_t a0 = s.start & ~uint64_t(15);
-  uint32_t reg;  // register after the main region (or ~init if none)
-  if (hn >= 16u) {
-    const uint32_t pad = kSegChunks - (hn >> 4);
+// Per-lane select between the two groups' uniform values.
+template <typename T>
+__device__ __forceinline__ T gsel(bool hi, T v0, T v1) {
+  return hi ? v1 : v0;
+}
+
+// Issues this lane's K chunk loads of the segment pair.  Virtual chunk
+// v = G*k + gl (chain k of lane gl of the group) holds chunk q = v - pad of
+// the group's main region, so load k of the wave reads G consecutive chunks
+// per group.  Virtual chunks in front (q < 0) read chunk 0 instead (always
+// mapped: it holds the span's first byte); the chains they feed are
+// overwritten by the injection or zeroed before the fold.  A group without
+// a main region (or an invalid one) loads the 4 KiB at `dummy`, so EVERY
+// slot issues exactly K vector loads and the ring stays regular.
+template <int K0, int K1>
+__device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, const void* dummy,
+                                          u32x4 (&d)[K]) {
+  uint32_t pad_g[S];
+  uint64_t base_g[S];
+#pragma unroll
+  for (int g = 0; g < S; ++g) {
+    const uint32_t hn = static_cast<uint32_t>(s[g].start & 15u) + s[g].n;
+    const bool live = (s[g].flags & kSlotValid) && hn >= 16u;
+    pad_g[g] = live ? kSegChunks - (hn >> 4) : 0u;
+    base_g[g] = live ? (s[g].start & ~uint64_t(15)) : reinterpret_cast<uint64_t>(dummy);
+  }
+  const bool hi = lane >= static_cast<uint32_t>(G);
+  const uint32_t gl = lane & (G - 1);
+  const uint32_t pad = gsel(hi, pad_g[0], pad_g[1]);
+  g_u32x4* b = reinterpret_cast<g_u32x4*>(gsel(hi, base_g[0], base_g[1]));
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const uint32_t v = gl + G * k;
+    const uint32_t q = v > pad ? v - pad : 0u;
+    d[k] = __builtin_nontemporal_load(b + q);
+  }
+}
+
+// Fold the G*K stripe registers of each group into the group's segment
+// register.  r[k] of lane gl covers chunk G*k + gl, i.e. sits (K-1-k)*G*16
+// + (G-1-gl)*16 bytes before the segment end.  In-lane Horner over k first
+// (shift by G*16 = 512 B), then the butterfly over the group's lanes: DPP
+// row shifts for partners 1..8 lanes away, v_readlane for 16.  Returns the
+// per-lane value; group g's result is in lane g*G.
+__device__ __forceinline__ uint32_t fold_groups(uint32_t (&r)[K], uint32_t lane) {
+  static_assert(G == 32, "the butterfly is written for 32-lane groups");
+  uint32_t v = r[0];
+#pragma unroll
+  for (int k = 1; k < K; ++k) v = shift_xor<5>(v, r[k]);
+  uint32_t p = row_shl<1>(v);
+  if ((lane & 1u) == 0u) v = shift_xor<0>(v, p);
+  p = row_shl<2>(v);
+  if ((lane & 3u) == 0u) v = shift_xor<1>(v, p);
+  p = row_shl<4>(v);
+  if ((lane & 7u) == 0u) v = shift_xor<2>(v, p);
+  p = row_shl<8>(v);
+  if ((lane & 15u) == 0u) v = shift_xor<3>(v, p);
+  const uint32_t g16 = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t g48 = __builtin_amdgcn_readlane(v, 48);
+  if ((lane & 31u) == 0u) v = shift_xor<4>(v, lane ? g48 : g16);
+  return v;
+}
+
+// Feeds the ragged tail of a group's segment (uniform): bytes [o, e) of the
+// 16-byte chunk at e0.
+__device__ __forceinline__ uint32_t feed_tail(uint32_t s0, uint32_t reg, uint64_t e0, uint32_t o,
+                                              uint32_t e) {
+  const uint32_t* tp = reinterpret_cast<const uint32_t*>(e0);
+  uint32_t t[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t[j] = (4u * j < e) ? tp[j] : 0u;
+  uint32_t i = o;
+  if (o == 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (4u * j + 4u <= e) {
+        reg = feed_word(s0, reg, t[j]);
+        i += 4;
+      }
+  }
+  for (; i < e; ++i) {
+    const uint32_t wd = i < 4 ? t[0] : (i < 8 ? t[1] : (i < 12 ? t[2] : t[3]));
+    reg = feed_byte(s0, reg, (wd >> (8 * (i & 3))) & 0xffu);
+  }
+  return reg;
+}
+
+// Processes one segment pair whose chunks are in d (already waited for).
+// For each group: `chain` carries the crc from segment to segment of a
+// span; when the segment completes its span, crc[g] is the span's crc and
+// done[g] is set.
+//
+// As soon as a half of d has been fed, the loads of the ring's next segment
+// pair `nx` are issued into it, so they are in flight during the rest of
+// this pair and all of the other slot's.
+template <bool kReissue>
+__device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[K], uint32_t s0,
+                                            uint32_t lane, uint32_t (&chain)[S],
+                                            uint32_t (&crc)[S], bool (&done)[S],
+                                            const Slot (&nx)[S], const void* dummy) {
+  const bool hi = lane >= static_cast<uint32_t>(G);
+  const uint32_t gl = lane & (G - 1);
+  uint32_t init[S], h[S], hn[S];
+  bool main_g[S], fast = true, any_main = false;
+#pragma unroll
+  for (int g = 0; g < S; ++g) {
+    init[g] = (s[g].flags & kSlotFirst) ? s[g].init : chain[g];
+    h[g] = static_cast<uint32_t>(s[g].start & 15u);
+    hn[g] = h[g] + s[g].n;
+    main_g[g] = (s[g].flags & kSlotValid) && hn[g] >= 16u;
+    fast = fast && main_g[g] && h[g] == 0u && hn[g] == 4096u;
+    any_main = any_main || main_g[g];
+  }
+  uint32_t reg[S];
+#pragma unroll
+  for (int g = 0; g < S; ++g) reg[g] = ~init[g];
+  if (any_main) {
     uint32_t r[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) r[k] = 0u;
-    if (hn == 4096u && h == 0u) {
-      // fast path: a whole aligned 4 KiB segment; ~init enters at lane 0,
-      // chain 0, before any byte
-      if (lane == 0) r[0] = ~init;
-      feed_chunks<K>(s0, r, d);
+    // feed all chains; with kReissue, half by half, reloading each fed half
+    // of d with the next pair's loads
+    auto feed_all = [&]() {
+      if (kReissue) {
+        feed_chunks<0, K / 2>(s0, r, d);
+        issue_seg<0, K / 2>(nx, lane, dummy, d);
+        feed_chunks<K / 2, K>(s0, r, d);
+        issue_seg<K / 2, K>(nx, lane, dummy, d);
+      } else {
+        feed_chunks<0, K>(s0, r, d);
+      }
+    };
+    if (fast) {
+      // every group holds a whole aligned 4 KiB segment: ~init enters at
+      // the group's lane 0, chain 0, before any byte
+      if (gl == 0) r[0] = gsel(hi, ~init[0], ~init[1]);
+      feed_all();
     } else {
-      // general path: chunk 0 sits at virtual chunk `pad` (lane pad%64,
-      // chain pad/64): mask its first h bytes and inject ~init * x^(-8h) there
-      const uint32_t inj = (init == 0u) ? lds_ld(kLdsHead0 + (h << 2))
-                                        : unshift_bytes(s0, ~init, h);
-      const uint32_t m0 = h == 0 ? ~0u : (h >= 4 ? 0u : (~0u << (8 * h)));
-      const uint32_t m1 = h <= 4 ? ~0u : (h >= 8 ? 0u : (~0u << (8 * (h - 4))));
-      const uint32_t m2 = h <= 8 ? ~0u : (h >= 12 ? 0u : (~0u << (8 * (h - 8))));
-      const uint32_t m3 = h <= 12 ? ~0u : (~0u << (8 * (h - 12)));
-      const uint32_t l0 = pad & 63u, k0 = pad >> 6;
-      u32x4 e[K];
+      // general path: chunk 0 of a group sits at its virtual chunk `pad`
+      // (lane pad%G, chain pad/G): mask its first h bytes and inject
+      // ~init * x^(-8h) there.  A group without a main region gets
+      // pad = 256: all its chains are zeroed.
+      uint32_t pad_g[S], inj_g[S], m_g[S][4];
+#pragma unroll
+      for (int g = 0; g < S; ++g) {
+        pad_g[g] = main_g[g] ? kSegChunks - (hn[g] >> 4) : kSegChunks;
+        const uint32_t hh = h[g];
+        inj_g[g] = 0u;
+        if (main_g[g])
+          inj_g[g] = (init[g] == 0u) ? lds_ld(kLdsHead0 + (hh << 2))
+                                     : unshift_bytes(s0, ~init[g], hh);
+        m_g[g][0] = hh == 0 ? ~0u : (hh >= 4 ? 0u : (~0u << (8 * hh)));
+        m_g[g][1] = hh <= 4 ? ~0u : (hh >= 8 ? 0u : (~0u << (8 * (hh - 4))));
+        m_g[g][2] = hh <= 8 ? ~0u : (hh >= 12 ? 0u : (~0u << (8 * (hh - 8))));
+        m_g[g][3] = hh <= 12 ? ~0u : (~0u << (8 * (hh - 12)));
+      }
+      const uint32_t pad = gsel(hi, pad_g[0], pad_g[1]);
+      const uint32_t inj = gsel(hi, inj_g[0], inj_g[1]);
+      const uint32_t l0 = pad & (G - 1), k0 = pad / G;
+      const bool at0 = gl == l0;
+      const uint32_t m0 = gsel(hi, m_g[0][0], m_g[1][0]), m1 = gsel(hi, m_g[0][1], m_g[1][1]);
+      const uint32_t m2 = gsel(hi, m_g[0][2], m_g[1][2]), m3 = gsel(hi, m_g[0][3], m_g[1][3]);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        e[k] = d[k];
-        if (static_cast<uint32_t>(k) == k0 && lane == l0) {
-          e[k].x &= m0;
-          e[k].y &= m1;
-          e[k].z &= m2;
-          e[k].w &= m3;
+        if (at0 && static_cast<uint32_t>(k) == k0) {
+          d[k].x &= m0;
+          d[k].y &= m1;
+          d[k].z &= m2;
+          d[k].w &= m3;
           r[k] = inj;
         }
       }
-      feed_chunks<K>(s0, r, e);
+      feed_all();
       // chains of virtual chunks (in front of the span) carry garbage
 #pragma unroll
       for (int k = 0; k < K; ++k)
-        if (lane + 64u * k < pad) r[k] = 0u;
+        if (gl + G * static_cast<uint32_t>(k) < pad) r[k] = 0u;
     }
-    reg = fold_wave_c2<K>(r, lane);
-  } else {
-    reg = ~init;
-  }
-
-  // ragged tail: bytes [o, e) of the chunk at a0 + (hn & ~15)
-  const uint32_t e = hn & 15u;
-  if (e != 0u) {
-    const uint32_t o = hn < 16u ? h : 0u;
-    const uint64_t e0 = a0 + (hn & ~15u);
-    uint32_t t[4];
-#ifdef WIPDB_TAIL_ASM
-    tail_chunk(e0, t);  // the chunk holding `end` is mapped (it has span bytes)
-#else
-    {
-      const uint32_t* tp = reinterpret_cast<const uint32_t*>(e0);
+    const uint32_t v = fold_groups(r, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) t[j] = (4u * j < e) ? tp[j] : 0u;
-    }
-#endif
-    uint32_t i = o;
-    if (o == 0) {
+    for (int g = 0; g < S; ++g)
+      if (main_g[g]) reg[g] = __builtin_amdgcn_readlane(v, g * G);
+  } else if (kReissue) {
+    issue_seg<0, K>(nx, lane, dummy, d);
+  }
+  // ragged tails: bytes [o, e) of the chunk at a0 + (hn & ~15)
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        if (4u * j + 4u <= e) {
-          reg = feed_word(s0, reg, t[j]);
-          i += 4;
-        }
+  for (int g = 0; g < S; ++g) {
+    const uint32_t e = hn[g] & 15u;
+    if ((s[g].flags & kSlotValid) && e != 0u) {
+      const uint64_t e0 = (s[g].start & ~uint64_t(15)) + (hn[g] & ~15u);
+      reg[g] = uni(feed_tail(s0, reg[g], e0, hn[g] < 16u ? h[g] : 0u, e));
     }
-    for (; i < e; ++i) {
-      const uint32_t wd = i < 4 ? t[0] : (i < 8 ? t[1] : (i < 12 ? t[2] : t[3]));
-      reg = feed_byte(s0, reg, (wd >> (8 * (i & 3))) & 0xffu);
-    }
+    const uint32_t c = ~reg[g];
+    done[g] = (s[g].flags & kSlotLast) != 0u;
+    crc[g] = c;
+    if (!done[g]) chain[g] = c;
   }
-  const uint32_t c = ~reg;
-  if (s.flags & kSlotLast) {
-    crc = c;
-    return true;
-  }
-  chain = c;
-  return false;
 }
 
-// Per-wave output buffer: lane j holds the crc of the wave's (base + j)-th
-// span; one vector store per 64 spans (flush(first_ordinal, crc_lane,
-// nvalid) is called with all lanes active).
-struct OutBuf {
-  uint32_t v = 0;      // per lane
-  uint32_t fill = 0;   // uniform: lanes filled
-  uint64_t base = 0;   // uniform: wave-local ordinal of lane 0
-};
-
-// The wave loop: a register ring of WIPDB_RING_SLOTS slots (2 or 3).  While
-// segment j is processed, the loads of the next 1 or 2 segments are in
-// flight (4-8 KiB per wave, 64-128 KiB per CU, ahead of the compute).  Every
-// step issues exactly 4 loads.
-template <int K, typename Src, typename Flush>
-__device__ __forceinline__ void run_waves(Src& src, uint64_t first_span, uint64_t span_stride,
-                                          const void* dummy, Flush flush) {
-  static_assert(K == 4, "the ring is written for 4 chunks per lane");
+// The wave loop over segment pairs (one segment per group).  emit(span,
+// crc, g) is called for every finished span, with all lanes active (span
+// and crc uniform).
+template <typename Src, typename Emit>
+__device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t waves,
+                                          const void* dummy, Emit emit) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l4 = (threadIdx.x & 31u) * 4u;
-  const uint32_t s0 = l4 | ((l4 | 0x80u) << 8) | (1u << 16);
-  if (first_span >= src.count) return;
+  const uint32_t s0 = l4 | ((l4 | 0x80u) << 8) | (1u << 24);
+  const uint64_t stride = waves * S;
 
-  SegCursor<Src> cur;
-  cur.begin(src, first_span, span_stride, lane);
-  uint32_t chain = 0;
-  OutBuf ob;
+  src.reset();
+  SegCursor<Src> cur[S];
+  uint32_t chain[S];
+  uint32_t live = 0;  // groups with spans left (checked once: all zero -> return)
+#pragma unroll
+  for (int g = 0; g < S; ++g) {
+    cur[g].begin(src, g, wave * S + g, stride, lane);
+    chain[g] = 0;
+    live |= cur[g].left;
+  }
+  if (live == 0u) return;
 
-  auto finish = [&](const Slot& sl, u32x4 (&d)[4]) {
-    uint32_t crc = 0;
-    if (process_seg<K>(sl, d, s0, lane, chain, crc)) {
-#if WIPDB_OUTBUF
-      ob.v = (lane == ob.fill) ? crc : ob.v;
-      if (++ob.fill == 64u) {
-        flush(ob.base, ob.v, 64u);
-        ob.base += 64u;
-        ob.fill = 0u;
-      }
-#else
-      flush(ob.base, crc, 1u);
-      ob.base += 1u;
-#endif
-    }
+  auto next = [&](Slot (&sl)[S]) {
+#pragma unroll
+    for (int g = 0; g < S; ++g) sl[g] = cur[g].next(src, g, lane);
+  };
+  auto valid = [](const Slot (&sl)[S]) {
+    uint32_t f = 0;
+#pragma unroll
+    for (int g = 0; g < S; ++g) f |= sl[g].flags;
+    return (f & kSlotValid) != 0u;
+  };
+#if WIPDB_EARLY_REISSUE
+  auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[K], const Slot (&nx)[S]) {
+    uint32_t crc[S];
+    bool done[S];
+    process_seg<true>(sl, d, s0, lane, chain, crc, done, nx, dummy);
+#pragma unroll
+    for (int g = 0; g < S; ++g)
+      if (done[g]) emit(sl[g].span, crc[g], g);
   };
 
-#if WIPDB_RING_SLOTS == 3
-  u32x4 bA[4], bB[4], bC[4];
-  Slot sA = cur.next(src, lane);
-  issue_seg(sA, lane, dummy, bA);
-  Slot sB = cur.next(src, lane);
-  issue_seg(sB, lane, dummy, bB);
+  // Two slots.  Slot A's data is reloaded with the pair after B while A is
+  // processed (half by half), so the loads of the next two pairs are in
+  // flight during each pair's compute.
+  Slot sA[S], sB[S], sN[S];
+  u32x4 bA[K], bB[K];
+  next(sA);
+  issue_seg<0, K>(sA, lane, dummy, bA);
+  next(sB);
+  issue_seg<0, K>(sB, lane, dummy, bB);
   for (;;) {
-    Slot sC = cur.next(src, lane);
-    issue_seg(sC, lane, dummy, bC);
-    if (!(sA.flags & kSlotValid)) break;
-    finish(sA, bA);
-
-    sA = cur.next(src, lane);
-    issue_seg(sA, lane, dummy, bA);
-    if (!(sB.flags & kSlotValid)) break;
-    finish(sB, bB);
-
-    sB = cur.next(src, lane);
-    issue_seg(sB, lane, dummy, bB);
-    if (!(sC.flags & kSlotValid)) break;
-    finish(sC, bC);
+    if (!valid(sA)) break;  // segments come in order: B is invalid too
+    next(sN);
+    finish(sA, bA, sN);
+#pragma unroll
+    for (int g = 0; g < S; ++g) sA[g] = sN[g];
+    if (!valid(sB)) break;
+    next(sN);
+    finish(sB, bB, sN);
+#pragma unroll
+    for (int g = 0; g < S; ++g) sB[g] = sN[g];
   }
 #else
-  // 2-slot ping-pong: one segment's loads in flight while one is computed
-  u32x4 bA[4], bB[4];
-  Slot sA = cur.next(src, lane);
-  issue_seg(sA, lane, dummy, bA);
+  auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[K]) {
+    uint32_t crc[S];
+    bool done[S];
+    process_seg<false>(sl, d, s0, lane, chain, crc, done, sl, dummy);
+#pragma unroll
+    for (int g = 0; g < S; ++g)
+      if (done[g]) emit(sl[g].span, crc[g], g);
+  };
+
+  // Two slots: while one pair is processed the other's loads are in flight.
+  Slot sA[S], sB[S];
+  u32x4 bA[K], bB[K];
+  next(sA);
+  issue_seg<0, K>(sA, lane, dummy, bA);
   for (;;) {
-    Slot sB = cur.next(src, lane);
-    issue_seg(sB, lane, dummy, bB);
-    if (!(sA.flags & kSlotValid)) break;
+    next(sB);
+    issue_seg<0, K>(sB, lane, dummy, bB);
+    if (!valid(sA)) break;
     finish(sA, bA);
 
-    sA = cur.next(src, lane);
-    issue_seg(sA, lane, dummy, bA);
-    if (!(sB.flags & kSlotValid)) break;
+    next(sA);
+    issue_seg<0, K>(sA, lane, dummy, bA);
+    if (!valid(sB)) break;
     finish(sB, bB);
   }
 #endif
-  if (ob.fill) flush(ob.base, ob.v, ob.fill);
 }
 
 // Copy the device tables into LDS: main tables replicated 32x, the rest
@@ -560,11 +590,14 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t first_span, uint64_
 __device__ __forceinline__ void load_tables(uint8_t* lds, const DevTables* __restrict__ tab) {
   const uint32_t tid = threadIdx.x;
   const uint32_t nthr = blockDim.x;
-  for (uint32_t e4 = tid; e4 < 4096u; e4 += nthr) {  // entry e = b*64 + u*32 + lane
-    const uint32_t e = e4 * 4u;
-    const uint32_t b = e >> 6, u = (e >> 5) & 1u;
-    const uint32_t v = u ? tab->t0[b] : tab->t1[b];
-    *reinterpret_cast<u32x4*>(lds + kLdsMain + e * 4u) = u32x4{v, v, v, v};
+  // main: 4 tables x 256 bytes x 32 replicas; 4 consecutive replicas per store
+  for (uint32_t e4 = tid; e4 < 8192u; e4 += nthr) {
+    const uint32_t rep4 = e4 & 7u;          // replicas 4*rep4 .. 4*rep4+3
+    const uint32_t b = (e4 >> 3) & 255u;
+    const uint32_t t = e4 >> 11;            // 0..3
+    const uint32_t v = tab->t[t][b];
+    const uint32_t addr = kLdsMain + (t >> 1) * 65536u + b * 256u + (t & 1u) * 128u + rep4 * 16u;
+    *reinterpret_cast<u32x4*>(lds + addr) = u32x4{v, v, v, v};
   }
   const u32x4* src = reinterpret_cast<const u32x4*>(tab->shift);
   u32x4* dst = reinterpret_cast<u32x4*>(lds + kLdsShift);
@@ -580,6 +613,15 @@ __device__ __forceinline__ uint64_t wave_id() {
   return static_cast<uint64_t>(blockIdx.x) * kWaves + uni(threadIdx.x >> 6);
 }
 
+__device__ __forceinline__ uint64_t grid_waves() {
+  return static_cast<uint64_t>(gridDim.x) * kWaves;
+}
+
+// Stores one value per finished span: lane g*G writes group g's result.
+__device__ __forceinline__ bool group_leader(int g) {
+  return (threadIdx.x & 63u) == static_cast<uint32_t>(g * G);
+}
+
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
@@ -591,13 +633,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  DescSource src{base, offsets, lengths, inits, count, 0u, 0, 0, 0, 0, 64u};
+  DescSource src{base, offsets, lengths, inits, count, 0u, 0, 0, 0, {0, 0}};
   const bool msk = (flags & kFlagMask) != 0;
-  const uint64_t first = wave_id();
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves;
-  run_waves<kChains>(src, first, stride, tab, [&](uint64_t ord, uint32_t crc, uint32_t nvalid) {
-    const uint32_t lane = threadIdx.x & 63u;
-    if (lane < nvalid) out[first + (ord + lane) * stride] = msk ? mask_crc(crc) : crc;
+  run_waves(src, wave_id(), grid_waves(), tab, [&](uint64_t span, uint32_t crc, int g) {
+    if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
 }
 
@@ -610,11 +649,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
   load_tables(lds, tab);
   StridedSource src{base, stride_bytes, length, init, count};
   const bool msk = (flags & kFlagMask) != 0;
-  const uint64_t first = wave_id();
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves;
-  run_waves<kChains>(src, first, stride, tab, [&](uint64_t ord, uint32_t crc, uint32_t nvalid) {
-    const uint32_t lane = threadIdx.x & 63u;
-    if (lane < nvalid) out[first + (ord + lane) * stride] = msk ? mask_crc(crc) : crc;
+  run_waves(src, wave_id(), grid_waves(), tab, [&](uint64_t span, uint32_t crc, int g) {
+    if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
 }
 
@@ -626,13 +662,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  DescSource src{base, offsets, lengths, nullptr, count, 1u, 0, 0, 0, 0, 64u};
-  const uint64_t first = wave_id();
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves;
-  run_waves<kChains>(src, first, stride, tab, [&](uint64_t ord, uint32_t crc, uint32_t nvalid) {
-    const uint32_t lane = threadIdx.x & 63u;
-    if (lane < nvalid) {
-      const uint64_t s = first + (ord + lane) * stride;
+  DescSource src{base, offsets, lengths, nullptr, count, 1u, 0, 0, 0, {0, 0}};
+  run_waves(src, wave_id(), grid_waves(), tab, [&](uint64_t s, uint32_t crc, int g) {
+    if (group_leader(g)) {
       const uint8_t* t = base + offsets[s] + lengths[s] + 1;
       const uint32_t stored = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) |
                               (uint32_t(t[3]) << 24);

@@ -104,8 +104,7 @@ const wipdb::gf2::Tables& HostTables() {
 
 void BuildDevTables(DevTables* dt) {
   const auto& T = HostTables();
-  memcpy(dt->t0, T.t[0], sizeof(dt->t0));
-  memcpy(dt->t1, T.t[1], sizeof(dt->t1));
+  memcpy(dt->t, T.t, sizeof(dt->t));  // slicing-by-4: T.t[0..3]
   for (uint32_t j = 0; j < wipdb::dev::kNumShift; ++j)
     wipdb::gf2::BuildShiftTable(uint64_t(16) << j, dt->shift[j]);
   for (int i = 0; i < 256; ++i) dt->inv_top[i] = T.inv_top[i];
@@ -113,7 +112,7 @@ void BuildDevTables(DevTables* dt) {
 }
 
 int LaunchGrid(hcrc_ctx* ctx, size_t count) {
-  size_t need = (count + wipdb::dev::kWaves - 1) / wipdb::dev::kWaves;
+  size_t need = (count + wipdb::dev::kSpansPerWG - 1) / wipdb::dev::kSpansPerWG;
   size_t g = std::min<size_t>(need, size_t(ctx->num_cu));
   return static_cast<int>(std::max<size_t>(g, 1));
 }
