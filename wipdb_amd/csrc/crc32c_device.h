@@ -12,12 +12,12 @@ constexpr int kThreads = kWaves * 64;    // 1024 threads
 constexpr uint32_t kFlagMask = 0x2;      // == HCRC_MASK_OUTPUT
 
 // Spans in flight per wave: the wave is split into kGroups lane groups of
-// kGroupLanes lanes; each group CRCs its own span, kChains chains per lane,
-// so one segment (one load group) is kGroupLanes * kChains = 256 chunks =
-// 4 KiB per group.
+// kGroupLanes lanes; each group CRCs its own span, kChunksPerLane 16-byte
+// chunks per lane, so one segment (one load group) is kGroupLanes *
+// kChunksPerLane = 256 chunks = 4 KiB per group.
 constexpr int kGroups = 2;
-constexpr int kGroupLanes = 64 / kGroups;       // 32
-constexpr int kChains = 256 / kGroupLanes;      // 8
+constexpr int kGroupLanes = 64 / kGroups;          // 32
+constexpr int kChunksPerLane = 256 / kGroupLanes;  // 8
 constexpr int kSpansPerWG = kWaves * kGroups;   // spans a workgroup starts at once
 
 // Shift tables: multiply by x^(8 * 16 * 2^j) for j < kNumShift (16 B .. 1 KiB).

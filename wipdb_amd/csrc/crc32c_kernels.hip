@@ -44,8 +44,31 @@
 
 #include "crc32c_device.h"
 
-#ifndef WIPDB_EARLY_REISSUE
-#define WIPDB_EARLY_REISSUE 0
+// Build knobs (the defaults are the measured best; scripts/build_variant.sh
+// builds the others for comparison):
+//   WIPDB_CPC      16-byte chunks per chain (1 or 2)
+//   WIPDB_NT       nontemporal data loads (1) or plain (0)
+//   WIPDB_XCHG     C == 2 with coalesced loads + DPP pair exchange
+//   WIPDB_SLOTS    register-ring depth (2 or 3; 3 spills at K = 8)
+//   WIPDB_ILP      chains interleaved per feed step
+//   WIPDB_LOADONLY diagnostic: the loads and ring without the CRC work
+#ifndef WIPDB_NT
+#define WIPDB_NT 0
+#endif
+#ifndef WIPDB_LOADONLY
+#define WIPDB_LOADONLY 0
+#endif
+#ifndef WIPDB_SLOTS
+#define WIPDB_SLOTS 2
+#endif
+#ifndef WIPDB_ILP
+#define WIPDB_ILP 8
+#endif
+#ifndef WIPDB_XCHG
+#define WIPDB_XCHG 0
+#endif
+#ifndef WIPDB_CPC
+#define WIPDB_CPC 2
 #endif
 
 
@@ -57,10 +80,26 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
 typedef __attribute__((address_space(3))) const uint32_t l_u32;
 
-constexpr int G = kGroupLanes;  // lanes per group (32)
-constexpr int K = kChains;      // chains per lane (8)
-constexpr int S = kGroups;      // groups (spans) per wave (2)
-static_assert(G * K == 256 && S * G == 64, "a group segment is 256 chunks");
+constexpr int G = kGroupLanes;     // lanes per group (32)
+constexpr int NL = kChunksPerLane; // 16-byte loads per lane per segment (8)
+constexpr int C = WIPDB_CPC;       // consecutive chunks per chain
+constexpr int K = NL / C;          // chains per lane
+constexpr int S = kGroups;         // groups (spans) per wave (2)
+constexpr uint32_t kLogC = C == 1 ? 0 : (C == 2 ? 1 : 2);
+static_assert(G * NL == 256 && S * G == 64 && K * C == NL, "a group segment is 256 chunks");
+// WIPDB_XCHG (C == 2): loads stay fully coalesced (load i of lane gl reads
+// chunk G*i + gl) and a DPP exchange between lane pairs gives each lane two
+// consecutive chunks: even lane 2m of chain k owns chunks 64k + 2m, +1, odd
+// lane 2m+1 owns chunks 64k + 32 + 2m, +1.
+constexpr bool X = WIPDB_XCHG != 0;
+static_assert(!X || C == 2, "the exchange pairs two chunks per chain");
+
+// Virtual chunk (within the 256-chunk group segment) of chunk j of chain k
+// of lane gl.
+__device__ __forceinline__ uint32_t vchunk(uint32_t k, uint32_t gl, uint32_t j) {
+  if (X) return 64u * k + 32u * (gl & 1u) + 2u * (gl >> 1) + j;
+  return C * (gl + G * k) + j;
+}
 
 // ---------------------------------------------------------------------------
 // LDS helpers (dynamic LDS starts at address 0: no static __shared__ here)
@@ -99,23 +138,27 @@ __device__ __forceinline__ uint32_t feed_word(uint32_t s0, uint32_t r, uint32_t 
   return step4(s0, r ^ w, 0u);
 }
 
-// Feed one 16-byte chunk into each of the K chains (interleaved by word).
-// Feed one 16-byte chunk into each of chains [K0, K1) (interleaved by word,
-// so their lookups are in flight together).
-template <int K0, int K1>
-__device__ __forceinline__ void feed_chunks(uint32_t s0, uint32_t (&r)[K], const u32x4 (&d)[K]) {
-  constexpr int I = K1 - K0;
-  uint32_t x[I];
+// Feed the SUB-th chunk of every chain into it (chains interleaved by word,
+// so their lookups are in flight together).  Chain k's chunks are
+// d[k*C .. k*C + C).
+// WIPDB_ILP chains at a time (fewer: fewer registers hold lookup results).
+template <int SUB>
+__device__ __forceinline__ void feed_chunks(uint32_t s0, uint32_t (&r)[K], const u32x4 (&d)[NL]) {
+  constexpr int I = WIPDB_ILP < K ? WIPDB_ILP : K;
 #pragma unroll
-  for (int i = 0; i < I; ++i) x[i] = r[K0 + i] ^ d[K0 + i].x;
+  for (int k0 = 0; k0 < K; k0 += I) {
+    uint32_t x[I];
 #pragma unroll
-  for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[K0 + i].y);
+    for (int i = 0; i < I; ++i) x[i] = r[k0 + i] ^ d[(k0 + i) * C + SUB].x;
 #pragma unroll
-  for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[K0 + i].z);
+    for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[(k0 + i) * C + SUB].y);
 #pragma unroll
-  for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[K0 + i].w);
+    for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[(k0 + i) * C + SUB].z);
 #pragma unroll
-  for (int i = 0; i < I; ++i) r[K0 + i] = step4(s0, x[i], 0u);
+    for (int i = 0; i < I; ++i) x[i] = step4(s0, x[i], d[(k0 + i) * C + SUB].w);
+#pragma unroll
+    for (int i = 0; i < I; ++i) r[k0 + i] = step4(s0, x[i], 0u);
+  }
 }
 
 // Feed one byte (Sarwate step with this lane's T0 replica).
@@ -130,6 +173,39 @@ template <int N>
 __device__ __forceinline__ uint32_t row_shl(uint32_t v) {
   return static_cast<uint32_t>(
       __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x100 | N, 0xF, 0xF, true));
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x110 | N, 0xF, 0xF, true));
+}
+
+// WIPDB_XCHG: loads 2k, 2k+1 hold chunks 64k + gl and 64k + 32 + gl; after
+// the exchange lane 2m holds 64k + 2m, +1 and lane 2m+1 holds 64k + 32 + 2m,
+// +1 (as d[2k], d[2k+1]).
+// The select is done with a lane bit mask, not a conditional: a DPP read
+// must execute with its source lanes active, and hipcc sinks a DPP operand
+// of a per-lane ?: into an exec-masked branch (whose inactive source lanes
+// then read as 0).
+template <int NLx>
+__device__ __forceinline__ void exchange_pairs(u32x4 (&d)[NLx], uint32_t gl) {
+  const uint32_t m = 0u - (gl & 1u);  // all ones on odd lanes
+#pragma unroll
+  for (int k = 0; k < NLx / 2; ++k) {
+    const u32x4 a = d[2 * k], b = d[2 * k + 1];
+    u32x4 f, t;
+    f.x = a.x ^ ((a.x ^ row_shr<1>(b.x)) & m);
+    f.y = a.y ^ ((a.y ^ row_shr<1>(b.y)) & m);
+    f.z = a.z ^ ((a.z ^ row_shr<1>(b.z)) & m);
+    f.w = a.w ^ ((a.w ^ row_shr<1>(b.w)) & m);
+    t.x = b.x ^ ((b.x ^ row_shl<1>(a.x)) & ~m);
+    t.y = b.y ^ ((b.y ^ row_shl<1>(a.y)) & ~m);
+    t.z = b.z ^ ((b.z ^ row_shl<1>(a.z)) & ~m);
+    t.w = b.w ^ ((b.w ^ row_shl<1>(a.w)) & ~m);
+    d[2 * k] = f;
+    d[2 * k + 1] = t;
+  }
 }
 
 // r * x^(8 * 16 * 2^J) mod P, XOR p: 4 lookups in shift table J.  The table
@@ -298,17 +374,18 @@ __device__ __forceinline__ T gsel(bool hi, T v0, T v1) {
   return hi ? v1 : v0;
 }
 
-// Issues this lane's K chunk loads of the segment pair.  Virtual chunk
-// v = G*k + gl (chain k of lane gl of the group) holds chunk q = v - pad of
-// the group's main region, so load k of the wave reads G consecutive chunks
-// per group.  Virtual chunks in front (q < 0) read chunk 0 instead (always
-// mapped: it holds the span's first byte); the chains they feed are
-// overwritten by the injection or zeroed before the fold.  A group without
-// a main region (or an invalid one) loads the 4 KiB at `dummy`, so EVERY
-// slot issues exactly K vector loads and the ring stays regular.
-template <int K0, int K1>
+// Issues this lane's NL chunk loads of the segment pair.  Load i = k*C + j
+// is chunk j of chain k: virtual chunk v = C*(G*k + gl) + j, which holds
+// chunk q = v - pad of the group's main region; so load i of the wave reads
+// the chunks C*G*k + j + {0, C, 2C, ...} of each group (C = 1: G
+// consecutive chunks; C = 2: every other one, the next load the rest).
+// Virtual chunks in front (q < 0) read chunk 0 instead (always mapped: it
+// holds the span's first byte); the chains they feed are overwritten by the
+// injection or zeroed before the fold.  A group without a main region (or
+// an invalid one) loads the 4 KiB at `dummy`, so EVERY slot issues exactly
+// NL vector loads and the ring stays regular.
 __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, const void* dummy,
-                                          u32x4 (&d)[K]) {
+                                          u32x4 (&d)[NL]) {
   uint32_t pad_g[S];
   uint64_t base_g[S];
 #pragma unroll
@@ -323,35 +400,45 @@ __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, con
   const uint32_t pad = gsel(hi, pad_g[0], pad_g[1]);
   g_u32x4* b = reinterpret_cast<g_u32x4*>(gsel(hi, base_g[0], base_g[1]));
 #pragma unroll
-  for (int k = K0; k < K1; ++k) {
-    const uint32_t v = gl + G * k;
+  for (int i = 0; i < NL; ++i) {
+    const uint32_t v = X ? gl + G * i : vchunk(i / C, gl, i % C);
     const uint32_t q = v > pad ? v - pad : 0u;
-    d[k] = __builtin_nontemporal_load(b + q);
+#if WIPDB_NT
+    d[i] = __builtin_nontemporal_load(b + q);
+#else
+    d[i] = b[q];
+#endif
   }
 }
 
-// Fold the G*K stripe registers of each group into the group's segment
-// register.  r[k] of lane gl covers chunk G*k + gl, i.e. sits (K-1-k)*G*16
-// + (G-1-gl)*16 bytes before the segment end.  In-lane Horner over k first
-// (shift by G*16 = 512 B), then the butterfly over the group's lanes: DPP
-// row shifts for partners 1..8 lanes away, v_readlane for 16.  Returns the
-// per-lane value; group g's result is in lane g*G.
+// Fold the G*K chain registers of each group into the group's segment
+// register.  Chain k of lane gl covers chunks C*(G*k + gl) .. +C-1, i.e.
+// ends (K-1-k)*G*C*16 + (G-1-gl)*C*16 bytes before the segment end.
+// In-lane Horner over k first (shift by G*C*16 bytes), then the butterfly
+// over the group's lanes (shift by C*16*2^t): DPP row shifts for partners
+// 1..8 lanes away, v_readlane for 16.  Returns the per-lane value; group
+// g's result is in lane g*G.
 __device__ __forceinline__ uint32_t fold_groups(uint32_t (&r)[K], uint32_t lane) {
   static_assert(G == 32, "the butterfly is written for 32-lane groups");
+  constexpr uint32_t L = kLogC;
   uint32_t v = r[0];
 #pragma unroll
-  for (int k = 1; k < K; ++k) v = shift_xor<5>(v, r[k]);
+  for (int k = 1; k < K; ++k) v = shift_xor<5 + L>(v, r[k]);
+  // with the exchange, lane bit 0 is chain-position bit 4 and lane bits
+  // 1..4 are position bits 0..3: the partner distance of each level follows
+  constexpr uint32_t J0 = X ? 4 + L : 0 + L, J1 = X ? 0 + L : 1 + L, J2 = X ? 1 + L : 2 + L;
+  constexpr uint32_t J3 = X ? 2 + L : 3 + L, J4 = X ? 3 + L : 4 + L;
   uint32_t p = row_shl<1>(v);
-  if ((lane & 1u) == 0u) v = shift_xor<0>(v, p);
+  if ((lane & 1u) == 0u) v = shift_xor<J0>(v, p);
   p = row_shl<2>(v);
-  if ((lane & 3u) == 0u) v = shift_xor<1>(v, p);
+  if ((lane & 3u) == 0u) v = shift_xor<J1>(v, p);
   p = row_shl<4>(v);
-  if ((lane & 7u) == 0u) v = shift_xor<2>(v, p);
+  if ((lane & 7u) == 0u) v = shift_xor<J2>(v, p);
   p = row_shl<8>(v);
-  if ((lane & 15u) == 0u) v = shift_xor<3>(v, p);
+  if ((lane & 15u) == 0u) v = shift_xor<J3>(v, p);
   const uint32_t g16 = __builtin_amdgcn_readlane(v, 16);
   const uint32_t g48 = __builtin_amdgcn_readlane(v, 48);
-  if ((lane & 31u) == 0u) v = shift_xor<4>(v, lane ? g48 : g16);
+  if ((lane & 31u) == 0u) v = shift_xor<J4>(v, lane ? g48 : g16);
   return v;
 }
 
@@ -383,15 +470,9 @@ __device__ __forceinline__ uint32_t feed_tail(uint32_t s0, uint32_t reg, uint64_
 // For each group: `chain` carries the crc from segment to segment of a
 // span; when the segment completes its span, crc[g] is the span's crc and
 // done[g] is set.
-//
-// As soon as a half of d has been fed, the loads of the ring's next segment
-// pair `nx` are issued into it, so they are in flight during the rest of
-// this pair and all of the other slot's.
-template <bool kReissue>
-__device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[K], uint32_t s0,
+__device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], uint32_t s0,
                                             uint32_t lane, uint32_t (&chain)[S],
-                                            uint32_t (&crc)[S], bool (&done)[S],
-                                            const Slot (&nx)[S], const void* dummy) {
+                                            uint32_t (&crc)[S], bool (&done)[S]) {
   const bool hi = lane >= static_cast<uint32_t>(G);
   const uint32_t gl = lane & (G - 1);
   uint32_t init[S], h[S], hn[S];
@@ -408,32 +489,37 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[K], u
   uint32_t reg[S];
 #pragma unroll
   for (int g = 0; g < S; ++g) reg[g] = ~init[g];
+#if WIPDB_LOADONLY
+  // diagnostic: the same loads and ring, no CRC work (wrong results)
   if (any_main) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) x ^= d[i].x ^ d[i].y ^ d[i].z ^ d[i].w;
+    x = __builtin_amdgcn_readlane(x, 0) ^ __builtin_amdgcn_readlane(x, 32);
+#pragma unroll
+    for (int g = 0; g < S; ++g)
+      if (main_g[g]) reg[g] = x;
+  }
+  if (false) {
+#else
+  if (any_main) {
+#endif
     uint32_t r[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) r[k] = 0u;
-    // feed all chains; with kReissue, half by half, reloading each fed half
-    // of d with the next pair's loads
-    auto feed_all = [&]() {
-      if (kReissue) {
-        feed_chunks<0, K / 2>(s0, r, d);
-        issue_seg<0, K / 2>(nx, lane, dummy, d);
-        feed_chunks<K / 2, K>(s0, r, d);
-        issue_seg<K / 2, K>(nx, lane, dummy, d);
-      } else {
-        feed_chunks<0, K>(s0, r, d);
-      }
-    };
+    if (X) exchange_pairs(d, gl);
     if (fast) {
       // every group holds a whole aligned 4 KiB segment: ~init enters at
       // the group's lane 0, chain 0, before any byte
       if (gl == 0) r[0] = gsel(hi, ~init[0], ~init[1]);
-      feed_all();
+      feed_chunks<0>(s0, r, d);
+      if (C > 1) feed_chunks<(C > 1 ? 1 : 0)>(s0, r, d);
     } else {
       // general path: chunk 0 of a group sits at its virtual chunk `pad`
-      // (lane pad%G, chain pad/G): mask its first h bytes and inject
-      // ~init * x^(-8h) there.  A group without a main region gets
-      // pad = 256: all its chains are zeroed.
+      // (chain k0 = pad / (G*C), lane l0, sub-chunk j0): mask its first h
+      // bytes and inject ~init * x^(-8h) into the chain just before it.  A
+      // group without a main region gets pad = 256: all its chains are
+      // zeroed.
       uint32_t pad_g[S], inj_g[S], m_g[S][4];
 #pragma unroll
       for (int g = 0; g < S; ++g) {
@@ -450,32 +536,42 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[K], u
       }
       const uint32_t pad = gsel(hi, pad_g[0], pad_g[1]);
       const uint32_t inj = gsel(hi, inj_g[0], inj_g[1]);
-      const uint32_t l0 = pad & (G - 1), k0 = pad / G;
+      const uint32_t k0 = pad / (G * C), rem = pad % (G * C);
+      const uint32_t l0 = X ? ((rem & 31u) & ~1u) + (rem >> 5) : rem / C;
+      const uint32_t j0 = rem % C;
       const bool at0 = gl == l0;
       const uint32_t m0 = gsel(hi, m_g[0][0], m_g[1][0]), m1 = gsel(hi, m_g[0][1], m_g[1][1]);
       const uint32_t m2 = gsel(hi, m_g[0][2], m_g[1][2]), m3 = gsel(hi, m_g[0][3], m_g[1][3]);
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        if (at0 && static_cast<uint32_t>(k) == k0) {
-          d[k].x &= m0;
-          d[k].y &= m1;
-          d[k].z &= m2;
-          d[k].w &= m3;
-          r[k] = inj;
+      for (int i = 0; i < NL; ++i) {
+        if (at0 && static_cast<uint32_t>(i) == k0 * C + j0) {
+          d[i].x &= m0;
+          d[i].y &= m1;
+          d[i].z &= m2;
+          d[i].w &= m3;
         }
       }
-      feed_all();
-      // chains of virtual chunks (in front of the span) carry garbage
 #pragma unroll
       for (int k = 0; k < K; ++k)
-        if (gl + G * static_cast<uint32_t>(k) < pad) r[k] = 0u;
+        if (at0 && static_cast<uint32_t>(k) == k0 && j0 == 0u) r[k] = inj;
+      feed_chunks<0>(s0, r, d);
+      if (C > 1) {
+        // a chain whose first chunk is virtual: the register enters here
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (at0 && static_cast<uint32_t>(k) == k0 && j0 == 1u) r[k] = inj;
+        feed_chunks<(C > 1 ? 1 : 0)>(s0, r, d);
+      }
+      // chains made only of virtual chunks (in front of the span) carry
+      // garbage
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (vchunk(k, gl, C - 1) < pad) r[k] = 0u;
     }
     const uint32_t v = fold_groups(r, lane);
 #pragma unroll
     for (int g = 0; g < S; ++g)
       if (main_g[g]) reg[g] = __builtin_amdgcn_readlane(v, g * G);
-  } else if (kReissue) {
-    issue_seg<0, K>(nx, lane, dummy, d);
   }
   // ragged tails: bytes [o, e) of the chunk at a0 + (hn & ~15)
 #pragma unroll
@@ -525,60 +621,54 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
     for (int g = 0; g < S; ++g) f |= sl[g].flags;
     return (f & kSlotValid) != 0u;
   };
-#if WIPDB_EARLY_REISSUE
-  auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[K], const Slot (&nx)[S]) {
+  auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[NL]) {
     uint32_t crc[S];
     bool done[S];
-    process_seg<true>(sl, d, s0, lane, chain, crc, done, nx, dummy);
+    process_seg(sl, d, s0, lane, chain, crc, done);
 #pragma unroll
     for (int g = 0; g < S; ++g)
       if (done[g]) emit(sl[g].span, crc[g], g);
   };
 
-  // Two slots.  Slot A's data is reloaded with the pair after B while A is
-  // processed (half by half), so the loads of the next two pairs are in
-  // flight during each pair's compute.
-  Slot sA[S], sB[S], sN[S];
-  u32x4 bA[K], bB[K];
+#if WIPDB_SLOTS == 3
+  // Three slots: while one pair is processed the next two pairs' loads are
+  // in flight.
+  Slot sA[S], sB[S], sC[S];
+  u32x4 bA[NL], bB[NL], bC[NL];
   next(sA);
-  issue_seg<0, K>(sA, lane, dummy, bA);
+  issue_seg(sA, lane, dummy, bA);
   next(sB);
-  issue_seg<0, K>(sB, lane, dummy, bB);
+  issue_seg(sB, lane, dummy, bB);
   for (;;) {
-    if (!valid(sA)) break;  // segments come in order: B is invalid too
-    next(sN);
-    finish(sA, bA, sN);
-#pragma unroll
-    for (int g = 0; g < S; ++g) sA[g] = sN[g];
-    if (!valid(sB)) break;
-    next(sN);
-    finish(sB, bB, sN);
-#pragma unroll
-    for (int g = 0; g < S; ++g) sB[g] = sN[g];
-  }
-#else
-  auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[K]) {
-    uint32_t crc[S];
-    bool done[S];
-    process_seg<false>(sl, d, s0, lane, chain, crc, done, sl, dummy);
-#pragma unroll
-    for (int g = 0; g < S; ++g)
-      if (done[g]) emit(sl[g].span, crc[g], g);
-  };
-
-  // Two slots: while one pair is processed the other's loads are in flight.
-  Slot sA[S], sB[S];
-  u32x4 bA[K], bB[K];
-  next(sA);
-  issue_seg<0, K>(sA, lane, dummy, bA);
-  for (;;) {
-    next(sB);
-    issue_seg<0, K>(sB, lane, dummy, bB);
+    next(sC);
+    issue_seg(sC, lane, dummy, bC);
     if (!valid(sA)) break;
     finish(sA, bA);
 
     next(sA);
-    issue_seg<0, K>(sA, lane, dummy, bA);
+    issue_seg(sA, lane, dummy, bA);
+    if (!valid(sB)) break;
+    finish(sB, bB);
+
+    next(sB);
+    issue_seg(sB, lane, dummy, bB);
+    if (!valid(sC)) break;
+    finish(sC, bC);
+  }
+#else
+  // Two slots: while one pair is processed the other's loads are in flight.
+  Slot sA[S], sB[S];
+  u32x4 bA[NL], bB[NL];
+  next(sA);
+  issue_seg(sA, lane, dummy, bA);
+  for (;;) {
+    next(sB);
+    issue_seg(sB, lane, dummy, bB);
+    if (!valid(sA)) break;
+    finish(sA, bA);
+
+    next(sA);
+    issue_seg(sA, lane, dummy, bA);
     if (!valid(sB)) break;
     finish(sB, bB);
   }
