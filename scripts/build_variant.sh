@@ -8,8 +8,11 @@ NAME=$1; shift
 make -s -C "$ROOT/wipdb_amd/csrc" >/dev/null
 OUT="$ROOT/build/variants/$NAME"
 mkdir -p "$OUT"
+# KSRC: another kernel source (e.g. a committed version) built against the
+# in-tree headers
+KSRC=${KSRC:-$ROOT/wipdb_amd/csrc/crc32c_kernels.hip}
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 "$@" \
-  -c -o "$OUT/crc32c_kernels.o" "$ROOT/wipdb_amd/csrc/crc32c_kernels.hip"
+  -I"$ROOT/wipdb_amd/csrc" -c -o "$OUT/crc32c_kernels.o" "$KSRC"
 O="$ROOT/build/obj"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libhip_crc32c_batch.so" \
   "$OUT/crc32c_kernels.o" "$O/hcrc_api.o" "$O/crc32c_api.o" "$O/crc32c_cpu.o" -lpthread

@@ -64,6 +64,9 @@
 #ifndef WIPDB_ILP
 #define WIPDB_ILP 8
 #endif
+#ifndef WIPDB_OPAQUE_LANE
+#define WIPDB_OPAQUE_LANE 1
+#endif
 #ifndef WIPDB_XCHG
 #define WIPDB_XCHG 0
 #endif
@@ -249,12 +252,14 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) {
 constexpr uint32_t kSegChunks = 256;
 constexpr uint32_t kSlotFirst = 1u, kSlotLast = 2u, kSlotValid = 4u;
 
+// Kept small: the ring holds several slots per group in SGPRs.
 struct Slot {
-  uint64_t span;   // span index (output slot)
   uint64_t start;  // first byte (absolute address)
-  uint32_t n;      // bytes in this segment
   uint32_t init;   // span init (first segment only)
-  uint32_t flags;  // kSlotFirst | kSlotLast | kSlotValid
+  uint32_t meta;   // bytes in this segment | flags << 16
+  uint32_t ord;    // the group's span ordinal (output index = first + ord * stride)
+  __device__ __forceinline__ uint32_t n() const { return meta & 0xffffu; }
+  __device__ __forceinline__ uint32_t flags() const { return meta >> 16; }
 };
 
 // ---------------------------------------------------------------------------
@@ -326,39 +331,40 @@ struct StridedSource {
 // segments in order -- the load side of the pipeline.
 template <typename Src>
 struct SegCursor {
-  uint64_t span, start, stride;
+  uint64_t start;
   uint32_t rest, init, first, left;  // left: spans not yet finished, incl. this one
+  uint32_t ord;                      // ordinal of the current span
 
-  __device__ __forceinline__ void begin(Src& src, int g, uint64_t s, uint64_t str,
+  __device__ __forceinline__ void begin(Src& src, int g, uint64_t s, uint64_t stride,
                                        uint32_t lane) {
-    stride = str;
-    span = s;
-    // s < str always, so this is ceil((count - s) / str) or 0 -- no compare
-    left = static_cast<uint32_t>((src.count + str - 1 - s) / str);
+    // s < stride always, so this is ceil((count - s) / stride) or 0 -- no compare
+    left = static_cast<uint32_t>((src.count + stride - 1 - s) / stride);
     first = 1u;
+    ord = 0u;
     start = 0;
     rest = 0;
     init = 0;
     if (left != 0u) src.desc(g, s, stride, lane, start, rest, init);
   }
-  __device__ __forceinline__ Slot next(Src& src, int g, uint32_t lane) {
+  __device__ __forceinline__ Slot next(Src& src, int g, uint64_t s0, uint64_t stride,
+                                       uint32_t lane) {
     // every field defined on every path (undef fields let LLVM substitute
     // another slot's value at the ring's merge points)
-    Slot sl{0, 0, 0, 0, 0};
+    Slot sl{0, 0, 0, 0};
     if (left == 0u) return sl;
     const uint32_t room = 4096u - static_cast<uint32_t>(start & 15u);
     const bool last = rest <= room;
     const uint32_t n = last ? rest : room;
-    sl.span = span;
     sl.start = start;
-    sl.n = n;
     sl.init = init;
-    sl.flags = kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u);
+    sl.meta = n | ((kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u)) << 16);
+    sl.ord = ord;
     if (last) {
-      span += stride;
+      ++ord;
       first = 1u;
       --left;
-      if (left != 0u) src.desc(g, span, stride, lane, start, rest, init);
+      if (left != 0u) src.desc(g, s0 + static_cast<uint64_t>(ord) * stride, stride, lane, start,
+                               rest, init);
     } else {
       start += n;
       rest -= n;
@@ -390,8 +396,8 @@ __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, con
   uint64_t base_g[S];
 #pragma unroll
   for (int g = 0; g < S; ++g) {
-    const uint32_t hn = static_cast<uint32_t>(s[g].start & 15u) + s[g].n;
-    const bool live = (s[g].flags & kSlotValid) && hn >= 16u;
+    const uint32_t hn = static_cast<uint32_t>(s[g].start & 15u) + s[g].n();
+    const bool live = (s[g].flags() & kSlotValid) && hn >= 16u;
     pad_g[g] = live ? kSegChunks - (hn >> 4) : 0u;
     base_g[g] = live ? (s[g].start & ~uint64_t(15)) : reinterpret_cast<uint64_t>(dummy);
   }
@@ -479,10 +485,10 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], 
   bool main_g[S], fast = true, any_main = false;
 #pragma unroll
   for (int g = 0; g < S; ++g) {
-    init[g] = (s[g].flags & kSlotFirst) ? s[g].init : chain[g];
+    init[g] = (s[g].flags() & kSlotFirst) ? s[g].init : chain[g];
     h[g] = static_cast<uint32_t>(s[g].start & 15u);
-    hn[g] = h[g] + s[g].n;
-    main_g[g] = (s[g].flags & kSlotValid) && hn[g] >= 16u;
+    hn[g] = h[g] + s[g].n();
+    main_g[g] = (s[g].flags() & kSlotValid) && hn[g] >= 16u;
     fast = fast && main_g[g] && h[g] == 0u && hn[g] == 4096u;
     any_main = any_main || main_g[g];
   }
@@ -577,12 +583,12 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], 
 #pragma unroll
   for (int g = 0; g < S; ++g) {
     const uint32_t e = hn[g] & 15u;
-    if ((s[g].flags & kSlotValid) && e != 0u) {
+    if ((s[g].flags() & kSlotValid) && e != 0u) {
       const uint64_t e0 = (s[g].start & ~uint64_t(15)) + (hn[g] & ~15u);
       reg[g] = uni(feed_tail(s0, reg[g], e0, hn[g] < 16u ? h[g] : 0u, e));
     }
     const uint32_t c = ~reg[g];
-    done[g] = (s[g].flags & kSlotLast) != 0u;
+    done[g] = (s[g].flags() & kSlotLast) != 0u;
     crc[g] = c;
     if (!done[g]) chain[g] = c;
   }
@@ -613,21 +619,28 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 
   auto next = [&](Slot (&sl)[S]) {
 #pragma unroll
-    for (int g = 0; g < S; ++g) sl[g] = cur[g].next(src, g, lane);
+    for (int g = 0; g < S; ++g) sl[g] = cur[g].next(src, g, wave * S + g, stride, lane);
   };
   auto valid = [](const Slot (&sl)[S]) {
     uint32_t f = 0;
 #pragma unroll
-    for (int g = 0; g < S; ++g) f |= sl[g].flags;
-    return (f & kSlotValid) != 0u;
+    for (int g = 0; g < S; ++g) f |= sl[g].meta;
+    return (f & (kSlotValid << 16)) != 0u;
   };
   auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[NL]) {
     uint32_t crc[S];
     bool done[S];
-    process_seg(sl, d, s0, lane, chain, crc, done);
+    // an opaque copy of the lane id: the lane predicates derived from it
+    // are recomputed per segment (one v_cmp each) instead of being hoisted
+    // into SGPR pairs that the register allocator then spills
+    uint32_t ln = lane;
+#if WIPDB_OPAQUE_LANE
+    asm volatile("" : "+v"(ln));
+#endif
+    process_seg(sl, d, s0, ln, chain, crc, done);
 #pragma unroll
     for (int g = 0; g < S; ++g)
-      if (done[g]) emit(sl[g].span, crc[g], g);
+      if (done[g]) emit(wave * S + g + static_cast<uint64_t>(sl[g].ord) * stride, crc[g], g);
   };
 
 #if WIPDB_SLOTS == 3
