@@ -58,6 +58,10 @@ def parse():
     p.add_argument("--stride", type=int, default=BLOCK,
                    help="diagnostic: block stride (0 = every block reads the same 4 KiB, "
                         "i.e. cache-resident compute ceiling); the headline uses 4096")
+    p.add_argument("--order", choices=["natural", "group", "cu"], default="natural",
+                   help="diagnostic: which block each descriptor names (natural: block i; "
+                        "group: every lane group sweeps its own contiguous run; cu: every "
+                        "workgroup sweeps its own contiguous region)")
     return p.parse_args()
 
 
@@ -154,7 +158,19 @@ def main():
     data = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     eng.fill_splitmix64_device(data, SEED, first_word=first * BLOCK // 8, stream=stream.cuda_stream)
-    offs = torch.arange(nblk, dtype=torch.int64, device=dev) * a.stride
+    idx = torch.arange(nblk, dtype=torch.int64, device=dev)
+    if a.order != "natural":
+        # span s is taken by lane group q = s % G at step k = s // G of the
+        # persistent grid (G = groups in the grid)
+        G = torch.cuda.get_device_properties(dev).multi_processor_count * 16 * 2
+        assert nblk % G == 0, "diagnostic orders need blocks divisible by the grid's groups"
+        q, k = idx % G, idx // G
+        if a.order == "group":
+            idx = q * (nblk // G) + k
+        else:
+            per_wg = 2 * 16  # groups per workgroup
+            idx = (q // per_wg) * (nblk // (G // per_wg)) + k * per_wg + q % per_wg
+    offs = idx * a.stride
     lens = torch.full((nblk,), BLOCK, dtype=torch.int32, device=dev)
     out = torch.empty(nblk, dtype=torch.int32, device=dev)
 
@@ -235,6 +251,9 @@ def main():
         }
         if rs:
             line["readstream_ceiling"] = rs
+        if a.order != "natural":
+            line["config"]["diagnostic_order"] = a.order
+            line["metric"] += " [DIAGNOSTIC order]"
         if a.stride != BLOCK:
             line["config"]["diagnostic_stride"] = a.stride
             line["metric"] += " [DIAGNOSTIC stride, not the headline]"

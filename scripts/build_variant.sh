@@ -14,6 +14,9 @@ KSRC=${KSRC:-$ROOT/wipdb_amd/csrc/crc32c_kernels.hip}
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 "$@" \
   -I"$ROOT/wipdb_amd/csrc" -c -o "$OUT/crc32c_kernels.o" "$KSRC"
 O="$ROOT/build/obj"
+# the launcher sees the same knobs (block size, table window)
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 "$@" \
+  -I"$ROOT/wipdb_amd/csrc" -x hip -c -o "$OUT/hcrc_api.o" "$ROOT/wipdb_amd/csrc/hcrc_api.cc"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libhip_crc32c_batch.so" \
-  "$OUT/crc32c_kernels.o" "$O/hcrc_api.o" "$O/crc32c_api.o" "$O/crc32c_cpu.o" -lpthread
+  "$OUT/crc32c_kernels.o" "$OUT/hcrc_api.o" "$O/crc32c_api.o" "$O/crc32c_cpu.o" -lpthread
 echo "$OUT/libhip_crc32c_batch.so"

@@ -7,7 +7,10 @@
 namespace wipdb {
 namespace dev {
 
-constexpr int kWaves = 16;               // waves per workgroup (1 WG per CU)
+#ifndef WIPDB_WAVES
+#define WIPDB_WAVES 16
+#endif
+constexpr int kWaves = WIPDB_WAVES;      // waves per workgroup (1 WG per CU)
 constexpr int kThreads = kWaves * 64;    // 1024 threads
 constexpr uint32_t kFlagMask = 0x2;      // == HCRC_MASK_OUTPUT
 
@@ -20,14 +23,17 @@ constexpr int kGroupLanes = 64 / kGroups;          // 32
 constexpr int kChunksPerLane = 256 / kGroupLanes;  // 8
 constexpr int kSpansPerWG = kWaves * kGroups;   // spans a workgroup starts at once
 
-// Shift tables: multiply by x^(8 * 16 * 2^j) for j < kNumShift (16 B .. 1 KiB).
-constexpr uint32_t kNumShift = 7;
+// Shift tables: multiply by x^(8 * 16 * 2^j) for j < kNumShift (16 B .. 2 KiB)
+// in device memory; a kernel keeps the kLdsShiftTables of them it uses
+// (j = log2(chunks per chain) + 0..5) in LDS.
+constexpr uint32_t kNumShift = 8;
+constexpr uint32_t kLdsShiftTables = 6;
 
 // LDS map (bytes), 160 KiB = the whole CU:
-//  [0, 28 KiB)    shift tables: 7 x [4 byte positions][256] u32 -- below
+//  [0, 24 KiB)    shift tables: 6 x [4 byte positions][256] u32 -- below
 //                 64 KiB so a compile-time table base fits the 16-bit
 //                 ds_read offset field.
-//  [28 KiB, +1 KiB) inv_top (256 u32), then head0 (16 u32).
+//  [24 KiB, +1 KiB) inv_top (256 u32), then head0 (16 u32).
 //  [32 KiB, 160 KiB) slicing-by-4 tables T0..T3, 32 replicas: entry
 //                 (t, b, lane) at 32 KiB + (t >> 1) * 64 KiB + b * 256 +
 //                 (t & 1) * 128 + (lane & 31) * 4.  Lane l only ever reads
@@ -36,7 +42,7 @@ constexpr uint32_t kNumShift = 7;
 //                 [lane byte | table bit, data byte, table half, 0]; the
 //                 32 KiB rides in the ds_read offset field.
 constexpr uint32_t kLdsShift = 0;
-constexpr uint32_t kLdsInvTop = kLdsShift + kNumShift * 4096;   // 28 KiB
+constexpr uint32_t kLdsInvTop = kLdsShift + kLdsShiftTables * 4096;   // 24 KiB
 constexpr uint32_t kLdsHead0 = kLdsInvTop + 1024;
 constexpr uint32_t kLdsMain = 32768;
 constexpr uint32_t kLdsBytes = kLdsMain + 4 * 32768;            // 160 KiB

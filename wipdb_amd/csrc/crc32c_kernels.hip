@@ -52,6 +52,7 @@
 //   WIPDB_SLOTS    register-ring depth (2 or 3; 3 spills at K = 8)
 //   WIPDB_ILP      chains interleaved per feed step
 //   WIPDB_LOADONLY diagnostic: the loads and ring without the CRC work
+//   WIPDB_NOFOLD   diagnostic: the scan without the cross-chain fold
 #ifndef WIPDB_NT
 #define WIPDB_NT 0
 #endif
@@ -73,6 +74,12 @@
 #ifndef WIPDB_CPC
 #define WIPDB_CPC 2
 #endif
+#ifndef WIPDB_NOFOLD
+#define WIPDB_NOFOLD 0
+#endif
+#ifndef WIPDB_LEAN_ISSUE
+#define WIPDB_LEAN_ISSUE 1
+#endif
 
 
 
@@ -90,6 +97,7 @@ constexpr int K = NL / C;          // chains per lane
 constexpr int S = kGroups;         // groups (spans) per wave (2)
 constexpr uint32_t kLogC = C == 1 ? 0 : (C == 2 ? 1 : 2);
 static_assert(G * NL == 256 && S * G == 64 && K * C == NL, "a group segment is 256 chunks");
+static_assert(C == 1 || C == 2 || C == 4, "chunks per chain");
 // WIPDB_XCHG (C == 2): loads stay fully coalesced (load i of lane gl reads
 // chunk G*i + gl) and a DPP exchange between lane pairs gives each lane two
 // consecutive chunks: even lane 2m of chain k owns chunks 64k + 2m, +1, odd
@@ -216,8 +224,9 @@ __device__ __forceinline__ void exchange_pairs(u32x4 (&d)[NLx], uint32_t gl) {
 // each address is one v_lshlrev_b32_sdwa (byte select).
 template <uint32_t J>
 __device__ __forceinline__ uint32_t shift_xor(uint32_t r, uint32_t p) {
-  constexpr uint32_t base = kLdsShift + J * 4096u;
-  static_assert(J < kNumShift && base + 4096u <= 65536u, "ds_read offset field is 16 bits");
+  static_assert(J >= kLogC && J - kLogC < kLdsShiftTables, "shift table not kept in LDS");
+  constexpr uint32_t base = kLdsShift + (J - kLogC) * 4096u;
+  static_assert(base + 4096u <= 65536u, "ds_read offset field is 16 bits");
   return xor3(xor3(lds_ld(base + ((r & 0xffu) << 2)), lds_ld(base + 1024u + (((r >> 8) & 0xffu) << 2)),
                    lds_ld(base + 2048u + (((r >> 16) & 0xffu) << 2))),
               lds_ld(base + 3072u + ((r >> 24) << 2)), p);
@@ -405,6 +414,22 @@ __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, con
   const uint32_t gl = lane & (G - 1);
   const uint32_t pad = gsel(hi, pad_g[0], pad_g[1]);
   g_u32x4* b = reinterpret_cast<g_u32x4*>(gsel(hi, base_g[0], base_g[1]));
+#if WIPDB_LEAN_ISSUE
+  if (!X && (pad_g[0] | pad_g[1]) == 0u) {
+    // both groups' segments fill the whole chunk grid (the common case):
+    // one lane address, the 8 loads at immediate offsets (C*G*k + j chunks)
+    g_u32x4* bl = b + C * gl;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+#if WIPDB_NT
+      d[i] = __builtin_nontemporal_load(bl + (C * G * (i / C) + i % C));
+#else
+      d[i] = bl[C * G * (i / C) + i % C];
+#endif
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const uint32_t v = X ? gl + G * i : vchunk(i / C, gl, i % C);
@@ -428,6 +453,12 @@ __device__ __forceinline__ uint32_t fold_groups(uint32_t (&r)[K], uint32_t lane)
   static_assert(G == 32, "the butterfly is written for 32-lane groups");
   constexpr uint32_t L = kLogC;
   uint32_t v = r[0];
+#if WIPDB_NOFOLD
+  // diagnostic: no GF(2) fold (wrong results)
+#pragma unroll
+  for (int k = 1; k < K; ++k) v ^= r[k];
+  return v;
+#endif
 #pragma unroll
   for (int k = 1; k < K; ++k) v = shift_xor<5 + L>(v, r[k]);
   // with the exchange, lane bit 0 is chain-position bit 4 and lane bits
@@ -519,7 +550,9 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], 
       // the group's lane 0, chain 0, before any byte
       if (gl == 0) r[0] = gsel(hi, ~init[0], ~init[1]);
       feed_chunks<0>(s0, r, d);
-      if (C > 1) feed_chunks<(C > 1 ? 1 : 0)>(s0, r, d);
+      if constexpr (C > 1) feed_chunks<1>(s0, r, d);
+      if constexpr (C > 2) feed_chunks<2>(s0, r, d);
+      if constexpr (C > 3) feed_chunks<3>(s0, r, d);
     } else {
       // general path: chunk 0 of a group sits at its virtual chunk `pad`
       // (chain k0 = pad / (G*C), lane l0, sub-chunk j0): mask its first h
@@ -561,12 +594,24 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], 
       for (int k = 0; k < K; ++k)
         if (at0 && static_cast<uint32_t>(k) == k0 && j0 == 0u) r[k] = inj;
       feed_chunks<0>(s0, r, d);
-      if (C > 1) {
-        // a chain whose first chunk is virtual: the register enters here
+      // a chain whose first chunks are virtual: the register enters before
+      // its first real chunk j0
+      auto inject = [&](uint32_t j) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
-          if (at0 && static_cast<uint32_t>(k) == k0 && j0 == 1u) r[k] = inj;
-        feed_chunks<(C > 1 ? 1 : 0)>(s0, r, d);
+          if (at0 && static_cast<uint32_t>(k) == k0 && j0 == j) r[k] = inj;
+      };
+      if constexpr (C > 1) {
+        inject(1u);
+        feed_chunks<1>(s0, r, d);
+      }
+      if constexpr (C > 2) {
+        inject(2u);
+        feed_chunks<2>(s0, r, d);
+      }
+      if constexpr (C > 3) {
+        inject(3u);
+        feed_chunks<3>(s0, r, d);
       }
       // chains made only of virtual chunks (in front of the span) carry
       // garbage
@@ -702,9 +747,9 @@ __device__ __forceinline__ void load_tables(uint8_t* lds, const DevTables* __res
     const uint32_t addr = kLdsMain + (t >> 1) * 65536u + b * 256u + (t & 1u) * 128u + rep4 * 16u;
     *reinterpret_cast<u32x4*>(lds + addr) = u32x4{v, v, v, v};
   }
-  const u32x4* src = reinterpret_cast<const u32x4*>(tab->shift);
+  const u32x4* src = reinterpret_cast<const u32x4*>(tab->shift[kLogC]);
   u32x4* dst = reinterpret_cast<u32x4*>(lds + kLdsShift);
-  for (uint32_t i = tid; i < kNumShift * 256u; i += nthr) dst[i] = src[i];
+  for (uint32_t i = tid; i < kLdsShiftTables * 256u; i += nthr) dst[i] = src[i];
   uint32_t* inv = reinterpret_cast<uint32_t*>(lds + kLdsInvTop);
   for (uint32_t i = tid; i < 256u; i += nthr) inv[i] = tab->inv_top[i];
   uint32_t* hd = reinterpret_cast<uint32_t*>(lds + kLdsHead0);
