@@ -1,0 +1,126 @@
+// include/wipdb/table.h -- SST writing and verification with batched block
+// checksums.
+//
+// TableBuilder mirrors kv::TableBuilder (kv/src/include/kv/table_builder.h,
+// kv/src/table/table_builder.cc) and writes the identical bytes, but its
+// WriteRawBlock (table_builder.cc:183-202) no longer computes the trailer
+// CRC inline: it appends a placeholder trailer, records the span
+// (contents || type byte), and the CRCs of all pending blocks are computed
+// in ONE batch -- on the MI355X through the C-ABI (hcrc_batch), or on the
+// host -- and patched in right before the bytes leave the builder's buffer
+// (at most TableOptions::max_buffer_size, the WritableFileWriter buffer of
+// kv/src/include/kv/env.h:85, and at Finish).  FinishTables() finishes many
+// builders (one compaction's outputs) with a single batch.
+//
+// VerifyTable / VerifyTables are Table::Open(paranoid_checks) + a full
+// iteration with ReadOptions::verify_checksums (kv/src/table/table.cc:37-82,
+// format.cc:66-143), as batches: all index blocks in one batch, then every
+// data block of every table in one batch.  The status is the one the
+// reference reports for the same image; per-block results are returned too.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "wipdb/status.h"
+
+namespace wipdb {
+namespace table {
+
+// Where block checksums are computed.
+enum class CrcMode {
+  kInline = 0,     // per block, host CPU, at WriteRawBlock (the reference's schedule)
+  kBatchCpu = 1,   // deferred and batched, host CPU
+  kBatchGpu = 2,   // deferred and batched on the MI355X; a device error is a Status
+  kBatchAuto = 3,  // deferred and batched; MI355X when usable, else host
+};
+
+struct TableOptions {
+  size_t block_size = 4096;          // kv/src/util/options.cc:22
+  int block_restart_interval = 16;   // options.cc:23
+  int bloom_bits_per_key = 0;        // 0: no filter policy; else NewBloomFilterPolicy(bits)
+  size_t max_buffer_size = 4u << 20; // EnvOptions::writable_file_max_buffer_size (env.h:85)
+  CrcMode crc_mode = CrcMode::kBatchAuto;
+  int device = 0;                    // HIP device for the batched modes
+};
+
+// Destination of a table's bytes (the WritableFileWriter role).
+class TableSink {
+ public:
+  virtual ~TableSink() = default;
+  virtual Status Append(const char* data, size_t n) = 0;
+};
+
+class StringSink : public TableSink {
+ public:
+  Status Append(const char* data, size_t n) override {
+    contents.append(data, n);
+    return Status::OK();
+  }
+  std::string contents;
+};
+
+class TableBuilder {
+ public:
+  TableBuilder(const TableOptions& options, TableSink* sink);
+  ~TableBuilder();
+  TableBuilder(const TableBuilder&) = delete;
+  TableBuilder& operator=(const TableBuilder&) = delete;
+
+  // REQUIRES: key > every key added before (bytewise).
+  void Add(std::string_view key, std::string_view value);
+  void Flush();
+  Status Finish();
+  void Abandon();
+  Status status() const;
+  uint64_t NumEntries() const;
+  uint64_t FileSize() const;
+  // Blocks whose CRC was computed in a batch (deferred modes).
+  uint64_t BatchedBlocks() const;
+
+ private:
+  friend Status FinishTables(TableBuilder* const* builders, size_t n);
+  struct Rep;
+  Rep* rep_;
+};
+
+// Finish() for n builders sharing one TableOptions::crc_mode, with the CRCs
+// of all their still-buffered blocks computed in ONE batch.  Returns the
+// first non-OK status; every builder is finished either way.
+Status FinishTables(TableBuilder* const* builders, size_t n);
+
+// ---- verification ----
+enum class BlockKind : uint8_t { kData = 0, kIndex = 1, kMetaIndex = 2, kFilter = 3 };
+
+struct BlockCheck {
+  uint64_t offset;
+  uint64_t size;   // handle size (contents, without the 5-byte trailer)
+  BlockKind kind;
+  bool ok;         // trailer present and Unmask(stored) == crc32c(contents || type)
+};
+
+// ReadBlock(verify_checksums) over an in-memory table image (format.cc:66-143):
+// OK, "truncated block read", "block checksum mismatch", "bad block type",
+// "corrupted compressed block contents".  *contents views the block.
+Status ReadBlock(const char* image, size_t image_size, uint64_t offset, uint64_t size,
+                 bool verify_checksums, std::string_view* contents);
+
+// Table::Open(paranoid_checks = true) + iterating every data block with
+// verify_checksums = true; meta-index and filter blocks are verified too but,
+// as in Table::ReadMeta (table.cc:84-138), their failures do not fail the
+// table.  blocks (optional) receives every block checked, in file order of
+// discovery.  bloom_bits_per_key > 0 reads the filter named by the policy.
+Status VerifyTable(const char* image, size_t image_size, int bloom_bits_per_key, CrcMode mode,
+                   int device, std::vector<BlockCheck>* blocks);
+
+// The same for many tables at once: one batch for the index blocks, one for
+// every other block.  statuses[i] is table i's status.
+Status VerifyTables(const char* const* images, const size_t* sizes, size_t n,
+                    int bloom_bits_per_key, CrcMode mode, int device,
+                    std::vector<Status>* statuses);
+
+}  // namespace table
+}  // namespace wipdb

@@ -1,0 +1,70 @@
+/* include/wipdb_sst.h -- C-ABI over the batched table / log layer
+ * (include/wipdb/table.h, include/wipdb/log.h), for FFI callers (the
+ * Python package binds it with ctypes, wipdb_amd/_lib.py).
+ *
+ * Status codes (the kv::Status a reference call returns for the same input):
+ *   WSST_OK            0   OK
+ *   WSST_CORRUPTION    1   Corruption other than a checksum mismatch
+ *   WSST_CRC_MISMATCH  2   Corruption("block checksum mismatch") /
+ *                          "checksum mismatch" (log records)
+ *   WSST_OTHER         3   any other non-OK status
+ *   WSST_ERR_*        <0   API errors (bad argument, buffer too small,
+ *                          device error under WSST_CRC_BATCH_GPU)
+ *
+ * crc_mode: WSST_CRC_INLINE (per block on the host, the reference's
+ * schedule), WSST_CRC_BATCH_CPU, WSST_CRC_BATCH_GPU (MI355X, errors are
+ * reported), WSST_CRC_BATCH_AUTO (MI355X when usable).
+ */
+#ifndef WIPDB_SST_H_
+#define WIPDB_SST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WSST_OK 0
+#define WSST_CORRUPTION 1
+#define WSST_CRC_MISMATCH 2
+#define WSST_OTHER 3
+#define WSST_ERR_INVALID (-1)
+#define WSST_ERR_TOO_SMALL (-2)
+#define WSST_ERR_DEVICE (-3)
+
+#define WSST_CRC_INLINE 0
+#define WSST_CRC_BATCH_CPU 1
+#define WSST_CRC_BATCH_GPU 2
+#define WSST_CRC_BATCH_AUTO 3
+
+/* Builds ntables tables with wipdb::table::TableBuilder (the reference's
+ * kv::TableBuilder format, kv/src/table/table_builder.cc): table t gets the
+ * next entries[t] (key, value) pairs (keys sorted within a table; blobs are
+ * concatenated, *_lens give the sizes).  The tables are finished together by
+ * FinishTables (one CRC batch).  Table t's bytes go to out[out_offsets[t],
+ * out_offsets[t] + sizes[t]) with tables packed back to back; cap bounds
+ * the total.  batched_blocks (nullable) receives the number of block CRCs
+ * computed in batches.  Returns a status code of the first failing table. */
+int wsst_build_tables(size_t ntables, const size_t* entries, const char* keys,
+                      const uint32_t* key_lens, const char* vals, const uint32_t* val_lens,
+                      int block_size, int restart_interval, int bloom_bits,
+                      size_t max_buffer_size, int crc_mode, int device, char* out,
+                      size_t cap, uint64_t* out_offsets, uint64_t* sizes,
+                      uint64_t* batched_blocks);
+
+/* ReadBlock(verify_checksums) on a table image (kv/src/table/format.cc:66). */
+int wsst_read_block(const char* image, size_t n, uint64_t offset, uint64_t size);
+
+/* Table::Open(paranoid_checks) + a verified iteration over n table images,
+ * the CRCs batched across all tables (kv/src/table/table.cc:37-138).
+ * codes[i] = table i's status code; returns the first non-OK code.
+ * bad_blocks (nullable) = blocks whose CRC failed, over all tables. */
+int wsst_verify_tables(const char* const* images, const size_t* sizes, size_t n,
+                       int bloom_bits, int crc_mode, int device, int* codes,
+                       uint64_t* blocks_checked, uint64_t* bad_blocks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WIPDB_SST_H_ */

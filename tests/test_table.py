@@ -1,0 +1,312 @@
+"""Batched table layer (SURVEY.md 8f-1 write side, 8f-2 read side) against the
+reference's own table code (oracle/_ref/libref_table.so: kv::TableBuilder,
+Table::Open, ReadBlock compiled from /root/reference/kv/src).
+
+Write side: the SST bytes of wipdb::table::TableBuilder -- block CRCs
+deferred and computed in batches -- equal kv::TableBuilder's bytes for the
+same (key, value) stream, over block sizes, restart intervals, bloom filters,
+mid-table buffer flushes and multi-table FinishTables.
+Read side: the batched verifier returns the reference's status for clean
+images and for seeded single-byte corruptions, and ReadBlock agrees block by
+block.  CPU modes run here; the MI355X modes are the `gpu` tests at the end.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from wipdb_amd import sst
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_TABLE_SO = os.path.join(REPO, "oracle", "_ref", "libref_table.so")
+
+
+class RefTable:
+    """ctypes view of oracle/_ref/libref_table.so (test infrastructure)."""
+
+    def __init__(self):
+        lib = ctypes.CDLL(REF_TABLE_SO)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        lib.ref_build_table.restype = ctypes.c_long
+        lib.ref_build_table.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, vp, sz]
+        lib.ref_verify_table.restype = ctypes.c_int
+        lib.ref_verify_table.argtypes = [vp, sz, ctypes.c_int, ctypes.POINTER(sz)]
+        lib.ref_read_block.restype = ctypes.c_int
+        lib.ref_read_block.argtypes = [vp, sz, ctypes.c_uint64, ctypes.c_uint64]
+        self.lib = lib
+
+    def build(self, kvs, block_size=4096, restart=16, bloom=0) -> bytes:
+        keys = b"".join(k for k, _ in kvs)
+        vals = b"".join(v for _, v in kvs)
+        kl = np.array([len(k) for k, _ in kvs] or [0], np.uint32)
+        vl = np.array([len(v) for _, v in kvs] or [0], np.uint32)
+        cap = 2 * (len(keys) + len(vals)) + 8192 + 64 * len(kvs)
+        out = ctypes.create_string_buffer(cap)
+        kb = ctypes.create_string_buffer(keys, len(keys) or 1)
+        vb = ctypes.create_string_buffer(vals, len(vals) or 1)
+        n = self.lib.ref_build_table(kb, kl.ctypes.data, vb, vl.ctypes.data, len(kvs),
+                                     block_size, restart, bloom, out, cap)
+        assert 0 < n <= cap
+        return out.raw[:n]
+
+    def verify(self, img: bytes, bloom=0) -> int:
+        b = ctypes.create_string_buffer(img, len(img) or 1)
+        nb = ctypes.c_size_t(0)
+        return int(self.lib.ref_verify_table(b, len(img), bloom, ctypes.byref(nb)))
+
+    def read_block(self, img: bytes, off: int, size: int) -> int:
+        b = ctypes.create_string_buffer(img, len(img) or 1)
+        return int(self.lib.ref_read_block(b, len(img), off, size))
+
+
+@pytest.fixture(scope="module")
+def ref_table():
+    if not os.path.exists(REF_TABLE_SO):
+        pytest.skip("oracle/_ref/libref_table.so not built (reference absent, no prebuilt copy)")
+    return RefTable()
+
+
+# ---- seeded (key, value) streams -------------------------------------------
+
+def kv_8binsert(n: int, seed: int):
+    """test_bench/8Binsert.sh shape: 16-byte user keys + 8-byte tag, 100-byte
+    printable values (CompressibleString-like, kv/src/util/testutil.cc:34-46)."""
+    rng = np.random.default_rng(seed)
+    user = np.unique(rng.integers(0, 2**63, size=n * 2, dtype=np.int64))[:n]
+    out = []
+    for i, u in enumerate(sorted(int(x) for x in user)):
+        tag = ((i + 1) << 8 | 1).to_bytes(8, "little")
+        key = b"%016x" % u + tag
+        val = bytes(rng.integers(32, 127, size=100, dtype=np.uint8))
+        out.append((key, val))
+    return out
+
+
+def kv_mixed(n: int, seed: int):
+    """Variable key/value sizes, long shared prefixes, 0xff bytes (separator
+    edge cases), empty values and values larger than a block."""
+    rng = np.random.default_rng(seed)
+    keys = set()
+    while len(keys) < n:
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            k = bytes(rng.integers(0, 256, size=int(rng.integers(1, 40)), dtype=np.uint8))
+        elif kind == 1:
+            k = b"common/prefix/" + bytes(rng.integers(97, 100, size=int(rng.integers(1, 12)),
+                                                       dtype=np.uint8))
+        elif kind == 2:
+            k = b"\xff" * int(rng.integers(1, 6)) + bytes([int(rng.integers(0, 256))])
+        else:
+            k = b"k%08d" % int(rng.integers(0, 10**8))
+        keys.add(k)
+    out = []
+    for k in sorted(keys):
+        r = rng.random()
+        vl = 0 if r < 0.05 else (int(rng.integers(4200, 9000)) if r < 0.08 else int(rng.integers(1, 300)))
+        out.append((k, bytes(rng.integers(0, 256, size=vl, dtype=np.uint8))))
+    return out
+
+
+CONFIGS = [
+    # (stream, n, seed, block_size, restart, bloom, max_buffer)
+    ("8binsert", 6000, 1, 4096, 16, 10, 4 << 20),
+    ("8binsert", 6000, 2, 4096, 16, 0, 4 << 20),
+    ("mixed", 3000, 3, 4096, 16, 10, 4 << 20),
+    ("mixed", 3000, 4, 1024, 1, 10, 64 << 10),   # buffer flushes mid-table
+    ("mixed", 2000, 5, 256, 4, 7, 4 << 20),
+    ("8binsert", 1, 6, 4096, 16, 10, 4 << 20),   # a single entry
+    ("8binsert", 0, 7, 4096, 16, 10, 4 << 20),   # an empty table
+]
+
+
+def _stream(kind, n, seed):
+    return kv_8binsert(n, seed) if kind == "8binsert" else kv_mixed(n, seed)
+
+
+# ---- write side -------------------------------------------------------------
+
+@pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[f"{c[0]}-{c[1]}-b{c[3]}-r{c[4]}-f{c[5]}" for c in CONFIGS])
+def test_table_bytes_equal_reference(ref_table, cfg, mode):
+    kind, n, seed, bs, rs, bloom, mb = cfg
+    kvs = _stream(kind, n, seed)
+    want = ref_table.build(kvs, bs, rs, bloom)
+    rc, imgs, batched = sst.build_tables([kvs], bs, rs, bloom, mb, mode)
+    assert rc == sst.OK
+    assert imgs[0] == want
+    if mode == sst.CRC_BATCH_CPU:
+        assert batched > 0
+    assert ref_table.verify(imgs[0], bloom) == 0
+
+
+def test_finish_tables_matches_one_by_one(ref_table):
+    """A compaction's outputs finished together (one CRC batch) are the same
+    files the reference writes one at a time."""
+    kvs = kv_8binsert(20000, 11)
+    tables = [kvs[i:i + 2500] for i in range(0, len(kvs), 2500)]
+    rc, imgs, batched = sst.build_tables(tables, bloom_bits=10, crc_mode=sst.CRC_BATCH_CPU)
+    assert rc == sst.OK and len(imgs) == len(tables)
+    for t, img in zip(tables, imgs):
+        assert img == ref_table.build(t, bloom=10)
+    assert batched == sum(len(_handles(img)) for img in imgs)
+
+
+# ---- read side --------------------------------------------------------------
+
+def _handles(img: bytes):
+    """(offset, size) of every block of a table image: data blocks from the
+    index, plus index, meta-index and filter (parsed in Python)."""
+    def varint(b, p):
+        r = s = 0
+        while True:
+            x = b[p]
+            p += 1
+            r |= (x & 0x7F) << s
+            s += 7
+            if x < 0x80:
+                return r, p
+
+    def entries(block):
+        nr = int.from_bytes(block[-4:], "little")
+        lim = len(block) - 4 * (nr + 1)
+        p, key, out = 0, b"", []
+        while p < lim:
+            sh, p = varint(block, p)
+            ns, p = varint(block, p)
+            vl, p = varint(block, p)
+            key = key[:sh] + block[p:p + ns]
+            out.append((key, block[p + ns:p + ns + vl]))
+            p += ns + vl
+        return out
+
+    f = img[-48:]
+    mo, p = varint(f, 0)
+    ms, p = varint(f, p)
+    io, p = varint(f, p)
+    isz, p = varint(f, p)
+    hs = [(mo, ms), (io, isz)]
+    for _, v in entries(img[io:io + isz]):
+        o, q = varint(v, 0)
+        s, q = varint(v, q)
+        hs.append((o, s))
+    for k, v in entries(img[mo:mo + ms]):
+        if k.startswith(b"filter."):
+            o, q = varint(v, 0)
+            s, q = varint(v, q)
+            hs.append((o, s))
+    return hs
+
+
+@pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
+def test_verify_clean_and_corrupted_match_reference(ref_table, mode):
+    kvs = kv_mixed(2500, 21)
+    img = ref_table.build(kvs, 1024, 16, 10)
+    assert sst.verify_tables([img], 10, mode)[0] == sst.OK
+    rng = np.random.default_rng(5)
+    body = len(img) - 48  # footer corruptions are checked separately
+    imgs, want = [], []
+    for pos in rng.integers(0, body, size=150):
+        b = bytearray(img)
+        b[int(pos)] ^= 1 << int(rng.integers(0, 8))
+        imgs.append(bytes(b))
+        want.append(ref_table.verify(bytes(b), 10))
+    # and inside every non-data block: index damage fails Open, meta-index
+    # and filter damage is ignored (Table::ReadMeta, table.cc:84-138)
+    for o, s in _handles(img)[:2] + _handles(img)[-1:]:
+        for d in (0, s // 2, s, s + 1):
+            b = bytearray(img)
+            b[o + d] ^= 0x20
+            imgs.append(bytes(b))
+            want.append(ref_table.verify(bytes(b), 10))
+    rc, codes = sst.verify_tables(imgs, 10, mode)
+    assert codes == want
+    assert sst.CRC_MISMATCH in want and sst.OK in want
+
+
+def test_verify_footer_and_truncation(ref_table):
+    img = ref_table.build(kv_8binsert(3000, 31), bloom=10)
+    cases = [img[:40], img[:-1], img[:len(img) // 2] + img[-48:]]
+    for pos in range(len(img) - 48, len(img)):
+        b = bytearray(img)
+        b[pos] ^= 0x40
+        cases.append(bytes(b))
+    _, codes = sst.verify_tables(cases, 10, sst.CRC_BATCH_CPU)
+    for c, got in zip(cases, codes):
+        want = ref_table.verify(c, 10)
+        assert (got == sst.OK) == (want == sst.OK), (len(c), got, want)
+
+
+def test_read_block_matches_reference(ref_table):
+    img = ref_table.build(kv_mixed(1500, 41), 2048, 16, 10)
+    hs = _handles(img)
+    rng = np.random.default_rng(9)
+    for o, s in hs:
+        assert sst.read_block(img, o, s) == ref_table.read_block(img, o, s) == sst.OK
+        for d in (-1, 1, 7):
+            assert sst.read_block(img, o + d, s) == ref_table.read_block(img, o + d, s)
+    for _ in range(200):
+        o, s = int(rng.integers(0, len(img))), int(rng.integers(0, 5000))
+        assert sst.read_block(img, o, s) == ref_table.read_block(img, o, s)
+
+
+def test_verify_many_tables_one_batch(ref_table):
+    tables = [kv_8binsert(1500, 100 + i) for i in range(12)]
+    imgs = [ref_table.build(t, bloom=10) for t in tables]
+    bad = bytearray(imgs[5])
+    bad[1000] ^= 4
+    imgs[5] = bytes(bad)
+    rc, codes, checked, nbad = sst.verify_tables(imgs, 10, sst.CRC_BATCH_CPU, count_blocks=True)
+    assert codes == [ref_table.verify(i, 10) for i in imgs]
+    assert codes[5] == sst.CRC_MISMATCH and rc == sst.CRC_MISMATCH
+    assert nbad == 1 and checked == sum(len(_handles(i)) for i in imgs)
+
+
+def test_c_abi_header_symbols_exported():
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    syms = sst.header_symbols()
+    assert set(syms) == set(sst._PROTOS)
+    assert all(hasattr(lib, s) for s in syms)
+
+
+# ---- MI355X ------------------------------------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", CONFIGS[:5], ids=[f"{c[0]}-{c[1]}-b{c[3]}" for c in CONFIGS[:5]])
+def test_gpu_table_bytes_equal_reference(ref_table, cfg, engine):
+    kind, n, seed, bs, rs, bloom, mb = cfg
+    kvs = _stream(kind, n, seed)
+    rc, imgs, batched = sst.build_tables([kvs], bs, rs, bloom, mb, sst.CRC_BATCH_GPU)
+    assert rc == sst.OK and batched > 0
+    assert imgs[0] == ref_table.build(kvs, bs, rs, bloom)
+
+
+@pytest.mark.gpu
+def test_gpu_compaction_outputs_one_batch(ref_table, engine):
+    """64 SSTs of ~2 MiB (8Binsert shape) finished in one MI355X batch."""
+    kvs = kv_8binsert(64 * 1200, 77)
+    tables = [kvs[i:i + 1200] for i in range(0, len(kvs), 1200)]
+    rc, imgs, batched = sst.build_tables(tables, bloom_bits=10, crc_mode=sst.CRC_BATCH_GPU)
+    assert rc == sst.OK
+    rc2, cpu_imgs, _ = sst.build_tables(tables, bloom_bits=10, crc_mode=sst.CRC_INLINE)
+    assert imgs == cpu_imgs
+    for i in (0, 31, 63):
+        assert imgs[i] == ref_table.build(tables[i], bloom=10)
+
+
+@pytest.mark.gpu
+def test_gpu_verify_matches_reference(ref_table, engine):
+    tables = [kv_mixed(1200, 200 + i) for i in range(6)]
+    imgs = [ref_table.build(t, 1024, 16, 10) for t in tables]
+    rng = np.random.default_rng(3)
+    for i in range(len(imgs)):
+        for _ in range(8):
+            b = bytearray(imgs[i])
+            b[int(rng.integers(0, len(b) - 48))] ^= 0x10
+            imgs.append(bytes(b))
+    rc, codes = sst.verify_tables(imgs, 10, sst.CRC_BATCH_GPU)
+    assert codes == [ref_table.verify(i, 10) for i in imgs]

@@ -1,0 +1,263 @@
+// table_builder.cc -- wipdb::table::TableBuilder: kv::TableBuilder's table
+// (kv/src/table/table_builder.cc) with the block-trailer CRCs computed in
+// batches, and the span-batch helper of span_crc.h.
+#include "../../include/wipdb/table.h"
+
+#include <algorithm>
+#include <memory>
+#include <string>
+
+#include "../../include/hip_crc32c_batch.h"
+#include "../../include/wipdb/crc32c.h"
+#include "span_crc.h"
+#include "sst_format.h"
+
+namespace wipdb {
+namespace cpu {
+uint32_t Extend(uint32_t init_crc, const void* data, size_t n);
+}  // namespace cpu
+
+namespace spancrc {
+
+Status Compute(const char* const* ptrs, const uint32_t* lens, size_t n, bool mask,
+               table::CrcMode mode, int device, uint32_t* out) {
+  if (n == 0) return Status::OK();
+  if (mode == table::CrcMode::kInline || mode == table::CrcMode::kBatchCpu) {
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t c = cpu::Extend(0, ptrs[i], lens[i]);
+      out[i] = mask ? kv::crc32c::Mask(c) : c;
+    }
+    return Status::OK();
+  }
+  // The batch entry takes one base and 64-bit offsets: base = lowest span.
+  const char* base = *std::min_element(ptrs, ptrs + n);
+  std::vector<uint64_t> offs(n);
+  for (size_t i = 0; i < n; ++i) offs[i] = static_cast<uint64_t>(ptrs[i] - base);
+  const auto policy = mode == table::CrcMode::kBatchGpu ? crc32c::BatchPolicy::kGpuOnly
+                                                        : crc32c::BatchPolicy::kAuto;
+  const int rc = crc32c::ExtendBatch(base, offs.data(), lens, nullptr, out, n, mask, policy,
+                                     device);
+  if (rc != HCRC_OK) return Status::IOError(std::string("hcrc batch: ") + hcrc_strerror(rc));
+  return Status::OK();
+}
+
+}  // namespace spancrc
+
+namespace table {
+
+using sst::Handle;
+
+struct TableBuilder::Rep {
+  TableOptions opt;
+  TableSink* sink;
+  uint64_t offset = 0;  // file offset of the next byte
+  Status status;
+  sst::BlockBuilder data_block;
+  sst::BlockBuilder index_block;
+  std::string last_key;
+  uint64_t num_entries = 0;
+  bool closed = false;
+  std::unique_ptr<sst::FilterBuilder> filter;
+  bool pending_index_entry = false;
+  Handle pending_handle;
+  // bytes not yet handed to the sink; buf[0] is at file offset buf_start
+  std::string buf;
+  // blocks in buf whose trailer CRC is still to be computed:
+  // (position of the contents in buf, contents size + 1 type byte)
+  std::vector<std::pair<size_t, uint32_t>> pending;
+  uint64_t batched_blocks = 0;
+
+  Rep(const TableOptions& o, TableSink* s)
+      : opt(o), sink(s), data_block(o.block_restart_interval), index_block(1) {
+    if (o.bloom_bits_per_key > 0) {
+      filter.reset(new sst::FilterBuilder(o.bloom_bits_per_key));
+      filter->StartBlock(0);
+    }
+  }
+
+  bool deferred() const { return opt.crc_mode != CrcMode::kInline; }
+
+  // kv TableBuilder::WriteRawBlock, with the CRC deferred in batched modes.
+  void WriteRawBlock(std::string_view contents, int type, Handle* h) {
+    h->offset = offset;
+    h->size = contents.size();
+    const size_t pos = buf.size();
+    buf.append(contents.data(), contents.size());
+    char trailer[sst::kBlockTrailerSize] = {static_cast<char>(type), 0, 0, 0, 0};
+    if (!deferred()) {
+      uint32_t crc = cpu::Extend(0, contents.data(), contents.size());
+      crc = cpu::Extend(crc, trailer, 1);
+      sst::EncodeFixed32(trailer + 1, kv::crc32c::Mask(crc));
+    } else {
+      pending.emplace_back(pos, static_cast<uint32_t>(contents.size() + 1));
+    }
+    buf.append(trailer, sizeof(trailer));
+    offset += contents.size() + sst::kBlockTrailerSize;
+    if (buf.size() >= opt.max_buffer_size) FlushBuffer();
+  }
+
+  void WriteBlock(sst::BlockBuilder* b, Handle* h) {
+    // Compression is not built into this library: a snappy-less reference
+    // build stores every block uncompressed with type 0 as well
+    // (table_builder.cc:137-151, port_posix.h:194-205).
+    WriteRawBlock(b->Finish(), sst::kNoCompression, h);
+    b->Reset();
+  }
+
+  // Patches the trailers of pending blocks from crcs and hands buf over.
+  void Drain(const uint32_t* crcs) {
+    for (size_t i = 0; i < pending.size(); ++i)
+      sst::EncodeFixed32(&buf[pending[i].first + pending[i].second], crcs[i]);
+    batched_blocks += pending.size();
+    pending.clear();
+    if (status.ok() && !buf.empty()) status = sink->Append(buf.data(), buf.size());
+    buf.clear();
+  }
+
+  void CollectSpans(std::vector<const char*>* p, std::vector<uint32_t>* l) const {
+    for (const auto& s : pending) {
+      p->push_back(buf.data() + s.first);
+      l->push_back(s.second);
+    }
+  }
+
+  void FlushBuffer() {
+    std::vector<const char*> p;
+    std::vector<uint32_t> l;
+    CollectSpans(&p, &l);
+    std::vector<uint32_t> crc(p.size());
+    Status s = spancrc::Compute(p.data(), l.data(), p.size(), true, opt.crc_mode, opt.device,
+                                crc.data());
+    if (!s.ok()) {
+      if (status.ok()) status = s;
+      pending.clear();
+      buf.clear();
+      return;
+    }
+    Drain(crc.data());
+  }
+
+  void Flush() {
+    if (!status.ok() || data_block.empty()) return;
+    WriteBlock(&data_block, &pending_handle);
+    if (status.ok()) pending_index_entry = true;
+    if (filter) filter->StartBlock(offset);
+  }
+
+  // kv TableBuilder::Finish without the final buffer hand-over.
+  void FinishBody() {
+    Flush();
+    closed = true;
+    Handle filter_h, meta_h, index_h;
+    if (status.ok() && filter) WriteRawBlock(filter->Finish(), sst::kNoCompression, &filter_h);
+    if (status.ok()) {
+      sst::BlockBuilder meta(opt.block_restart_interval);
+      if (filter) {
+        std::string enc;
+        filter_h.EncodeTo(&enc);
+        meta.Add(std::string("filter.") + sst::Bloom::Name(), enc);
+      }
+      WriteBlock(&meta, &meta_h);
+    }
+    if (status.ok()) {
+      if (pending_index_entry) {
+        sst::ShortSuccessor(&last_key);
+        std::string enc;
+        pending_handle.EncodeTo(&enc);
+        index_block.Add(last_key, enc);
+        pending_index_entry = false;
+      }
+      WriteBlock(&index_block, &index_h);
+    }
+    if (status.ok()) {
+      std::string footer;
+      sst::EncodeFooter(meta_h, index_h, &footer);
+      buf.append(footer);
+      offset += footer.size();
+    }
+  }
+};
+
+TableBuilder::TableBuilder(const TableOptions& options, TableSink* sink)
+    : rep_(new Rep(options, sink)) {}
+
+TableBuilder::~TableBuilder() { delete rep_; }
+
+void TableBuilder::Add(std::string_view key, std::string_view value) {
+  Rep* r = rep_;
+  if (r->closed || !r->status.ok()) return;
+  if (r->pending_index_entry) {
+    sst::ShortestSeparator(&r->last_key, key);
+    std::string enc;
+    r->pending_handle.EncodeTo(&enc);
+    r->index_block.Add(r->last_key, enc);
+    r->pending_index_entry = false;
+  }
+  if (r->filter) r->filter->AddKey(key);
+  r->last_key.assign(key.data(), key.size());
+  ++r->num_entries;
+  r->data_block.Add(key, value);
+  if (r->data_block.SizeEstimate() >= r->opt.block_size) r->Flush();
+}
+
+void TableBuilder::Flush() {
+  if (!rep_->closed) rep_->Flush();
+}
+
+Status TableBuilder::Finish() {
+  Rep* r = rep_;
+  if (r->closed) return Status::InvalidArgument("table already finished or abandoned");
+  r->FinishBody();
+  if (r->status.ok()) r->FlushBuffer();
+  return r->status;
+}
+
+void TableBuilder::Abandon() {
+  Rep* r = rep_;
+  if (r->closed) return;
+  r->closed = true;
+  // what was appended stays in the file, as with kv's WritableFileWriter
+  if (r->status.ok()) r->FlushBuffer();
+}
+
+Status TableBuilder::status() const { return rep_->status; }
+uint64_t TableBuilder::NumEntries() const { return rep_->num_entries; }
+uint64_t TableBuilder::FileSize() const { return rep_->offset; }
+uint64_t TableBuilder::BatchedBlocks() const { return rep_->batched_blocks; }
+
+Status FinishTables(TableBuilder* const* builders, size_t n) {
+  if (n == 0) return Status::OK();
+  const CrcMode mode = builders[0]->rep_->opt.crc_mode;
+  const int device = builders[0]->rep_->opt.device;
+  for (size_t i = 0; i < n; ++i)
+    if (builders[i]->rep_->opt.crc_mode != mode || builders[i]->rep_->opt.device != device)
+      return Status::InvalidArgument("FinishTables: builders differ in crc_mode/device");
+  std::vector<const char*> p;
+  std::vector<uint32_t> l;
+  std::vector<size_t> first(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    TableBuilder::Rep* r = builders[i]->rep_;
+    if (!r->closed) r->FinishBody();
+    first[i] = p.size();
+    if (r->status.ok()) r->CollectSpans(&p, &l);
+  }
+  first[n] = p.size();
+  std::vector<uint32_t> crc(p.size());
+  Status s = spancrc::Compute(p.data(), l.data(), p.size(), true, mode, device, crc.data());
+  Status result;
+  for (size_t i = 0; i < n; ++i) {
+    TableBuilder::Rep* r = builders[i]->rep_;
+    if (!s.ok() && r->status.ok()) r->status = s;
+    if (r->status.ok()) {
+      r->Drain(crc.data() + first[i]);
+    } else {
+      r->pending.clear();
+      r->buf.clear();
+    }
+    if (result.ok() && !r->status.ok()) result = r->status;
+  }
+  return result;
+}
+
+}  // namespace table
+}  // namespace wipdb

@@ -1,0 +1,121 @@
+// wsst_capi.cc -- the C-ABI of include/wipdb_sst.h over the C++ table layer.
+#include "../../include/wipdb_sst.h"
+
+#include <string.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/wipdb/table.h"
+
+namespace {
+
+using wipdb::Status;
+using wipdb::table::CrcMode;
+
+int Code(const Status& s) {
+  if (s.ok()) return WSST_OK;
+  if (s.code() == Status::kIOError && s.message().rfind("hcrc", 0) == 0) return WSST_ERR_DEVICE;
+  if (s.IsCorruption())
+    return s.message().find("checksum mismatch") != std::string::npos ? WSST_CRC_MISMATCH
+                                                                      : WSST_CORRUPTION;
+  return WSST_OTHER;
+}
+
+bool ModeOf(int m, CrcMode* out) {
+  if (m < WSST_CRC_INLINE || m > WSST_CRC_BATCH_AUTO) return false;
+  *out = static_cast<CrcMode>(m);
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wsst_build_tables(size_t ntables, const size_t* entries, const char* keys,
+                      const uint32_t* key_lens, const char* vals, const uint32_t* val_lens,
+                      int block_size, int restart_interval, int bloom_bits,
+                      size_t max_buffer_size, int crc_mode, int device, char* out,
+                      size_t cap, uint64_t* out_offsets, uint64_t* sizes,
+                      uint64_t* batched_blocks) {
+  CrcMode mode;
+  if (!ModeOf(crc_mode, &mode) || !entries || !out || !out_offsets || !sizes ||
+      block_size <= 0 || restart_interval <= 0 || max_buffer_size == 0)
+    return WSST_ERR_INVALID;
+  wipdb::table::TableOptions opt;
+  opt.block_size = static_cast<size_t>(block_size);
+  opt.block_restart_interval = restart_interval;
+  opt.bloom_bits_per_key = bloom_bits;
+  opt.max_buffer_size = max_buffer_size;
+  opt.crc_mode = mode;
+  opt.device = device;
+  std::vector<std::unique_ptr<wipdb::table::StringSink>> sinks(ntables);
+  std::vector<std::unique_ptr<wipdb::table::TableBuilder>> tbs(ntables);
+  std::vector<wipdb::table::TableBuilder*> raw(ntables);
+  size_t ko = 0, vo = 0, e = 0;
+  for (size_t t = 0; t < ntables; ++t) {
+    sinks[t].reset(new wipdb::table::StringSink);
+    tbs[t].reset(new wipdb::table::TableBuilder(opt, sinks[t].get()));
+    raw[t] = tbs[t].get();
+    for (size_t i = 0; i < entries[t]; ++i, ++e) {
+      tbs[t]->Add(std::string_view(keys + ko, key_lens[e]),
+                  std::string_view(vals + vo, val_lens[e]));
+      ko += key_lens[e];
+      vo += val_lens[e];
+    }
+  }
+  const Status s = wipdb::table::FinishTables(raw.data(), ntables);
+  uint64_t total = 0, batched = 0;
+  for (size_t t = 0; t < ntables; ++t) {
+    out_offsets[t] = total;
+    sizes[t] = sinks[t]->contents.size();
+    if (total + sizes[t] > cap) return WSST_ERR_TOO_SMALL;
+    memcpy(out + total, sinks[t]->contents.data(), sizes[t]);
+    total += sizes[t];
+    batched += tbs[t]->BatchedBlocks();
+  }
+  if (batched_blocks) *batched_blocks = batched;
+  return Code(s);
+}
+
+int wsst_read_block(const char* image, size_t n, uint64_t offset, uint64_t size) {
+  if (!image) return WSST_ERR_INVALID;
+  return Code(wipdb::table::ReadBlock(image, n, offset, size, true, nullptr));
+}
+
+int wsst_verify_tables(const char* const* images, const size_t* sizes, size_t n,
+                       int bloom_bits, int crc_mode, int device, int* codes,
+                       uint64_t* blocks_checked, uint64_t* bad_blocks) {
+  CrcMode mode;
+  if (!ModeOf(crc_mode, &mode) || (n && (!images || !sizes))) return WSST_ERR_INVALID;
+  uint64_t checked = 0, bad = 0;
+  int first = WSST_OK;
+  if (!blocks_checked && !bad_blocks) {
+    std::vector<Status> st;
+    const Status s = wipdb::table::VerifyTables(images, sizes, n, bloom_bits, mode, device, &st);
+    if (s.code() == Status::kIOError && st.empty()) return Code(s);
+    for (size_t i = 0; i < st.size(); ++i) {
+      if (codes) codes[i] = Code(st[i]);
+      if (first == WSST_OK) first = Code(st[i]);
+    }
+    return first;
+  }
+  // per-block accounting: one table at a time (still one batch per stage)
+  for (size_t i = 0; i < n; ++i) {
+    std::vector<wipdb::table::BlockCheck> b;
+    const Status s =
+        wipdb::table::VerifyTable(images[i], sizes[i], bloom_bits, mode, device, &b);
+    const int c = Code(s);
+    if (c == WSST_ERR_DEVICE) return c;
+    if (codes) codes[i] = c;
+    if (first == WSST_OK) first = c;
+    checked += b.size();
+    for (const auto& x : b) bad += x.ok ? 0 : 1;
+  }
+  if (blocks_checked) *blocks_checked = checked;
+  if (bad_blocks) *bad_blocks = bad;
+  return first;
+}
+
+}  // extern "C"

@@ -1,0 +1,121 @@
+"""Python mirror of the batched table layer (include/wipdb/table.h) through
+its C-ABI (include/wipdb_sst.h).
+
+    build_tables(tables, ...)   kv::TableBuilder's SST bytes, block CRCs in one batch
+    verify_tables(images, ...)  Table::Open(paranoid) + verified iteration, batched
+    read_block(image, off, n)   ReadBlock(verify_checksums)
+
+Status codes follow wipdb_sst.h: 0 OK, 1 corruption, 2 checksum mismatch,
+3 other; negative = API / device error (raised as SstError).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           "include", "wipdb_sst.h")
+
+OK, CORRUPTION, CRC_MISMATCH, OTHER = 0, 1, 2, 3
+ERR_INVALID, ERR_TOO_SMALL, ERR_DEVICE = -1, -2, -3
+CRC_INLINE, CRC_BATCH_CPU, CRC_BATCH_GPU, CRC_BATCH_AUTO = 0, 1, 2, 3
+
+_c = ctypes
+_vp, _sz = _c.c_void_p, _c.c_size_t
+_PROTOS = {
+    "wsst_build_tables": (_c.c_int, [_sz, _vp, _vp, _vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int,
+                                     _sz, _c.c_int, _c.c_int, _vp, _sz, _vp, _vp, _vp]),
+    "wsst_read_block": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64]),
+    "wsst_verify_tables": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_int, _c.c_int, _vp, _vp,
+                                      _vp]),
+}
+_bound = None
+
+
+class SstError(RuntimeError):
+    pass
+
+
+def header_symbols() -> list[str]:
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*]+\s+)+\**(wsst_\w+)\s*\(", text, re.M)))
+
+
+def _load():
+    global _bound
+    if _bound is None:
+        lib = _lib.load()
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _bound = lib
+    return _bound
+
+
+def _blob(items: Sequence[bytes]):
+    lens = np.fromiter((len(x) for x in items), dtype=np.uint32, count=len(items))
+    return b"".join(items), lens
+
+
+def build_tables(tables: Sequence[Sequence[tuple[bytes, bytes]]], block_size: int = 4096,
+                 restart_interval: int = 16, bloom_bits: int = 0,
+                 max_buffer_size: int = 4 << 20, crc_mode: int = CRC_BATCH_AUTO,
+                 device: int = 0) -> tuple[int, list[bytes], int]:
+    """Builds every table (a sorted list of (key, value)) and finishes them
+    together.  Returns (status code, table images, blocks CRC'd in batches)."""
+    lib = _load()
+    n = len(tables)
+    entries = np.array([len(t) for t in tables], dtype=np.uint64)
+    flat = [kv for t in tables for kv in t]
+    keys, klen = _blob([k for k, _ in flat])
+    vals, vlen = _blob([v for _, v in flat])
+    cap = 2 * (len(keys) + len(vals)) + 4096 * (n + 1) + 64 * len(flat)
+    out = _c.create_string_buffer(cap)
+    offs = np.zeros(max(n, 1), np.uint64)
+    sizes = np.zeros(max(n, 1), np.uint64)
+    batched = _c.c_uint64(0)
+    kbuf = _c.create_string_buffer(keys, len(keys) or 1)
+    vbuf = _c.create_string_buffer(vals, len(vals) or 1)
+    rc = lib.wsst_build_tables(n, entries.ctypes.data, kbuf, klen.ctypes.data, vbuf,
+                               vlen.ctypes.data, block_size, restart_interval, bloom_bits,
+                               max_buffer_size, crc_mode, device, out, cap, offs.ctypes.data,
+                               sizes.ctypes.data, _c.byref(batched))
+    if rc < 0:
+        raise SstError(f"wsst_build_tables: {rc}")
+    raw = out.raw
+    imgs = [raw[int(offs[i]):int(offs[i] + sizes[i])] for i in range(n)]
+    return rc, imgs, int(batched.value)
+
+
+def verify_tables(images: Sequence[bytes], bloom_bits: int = 0, crc_mode: int = CRC_BATCH_AUTO,
+                  device: int = 0, count_blocks: bool = False):
+    """Returns (first status code, per-table codes[, blocks checked, bad blocks])."""
+    lib = _load()
+    n = len(images)
+    bufs = [_c.create_string_buffer(im, len(im) or 1) for im in images]
+    ptrs = (_c.c_void_p * max(n, 1))(*[_c.addressof(b) for b in bufs])
+    sizes = np.array([len(im) for im in images] or [0], dtype=np.uint64)
+    codes = np.zeros(max(n, 1), np.int32)
+    chk, bad = _c.c_uint64(0), _c.c_uint64(0)
+    rc = lib.wsst_verify_tables(ptrs, sizes.ctypes.data, n, bloom_bits, crc_mode, device,
+                                codes.ctypes.data, _c.byref(chk) if count_blocks else None,
+                                _c.byref(bad) if count_blocks else None)
+    if rc < 0:
+        raise SstError(f"wsst_verify_tables: {rc}")
+    if count_blocks:
+        return rc, codes[:n].tolist(), int(chk.value), int(bad.value)
+    return rc, codes[:n].tolist()
+
+
+def read_block(image: bytes, offset: int, size: int) -> int:
+    lib = _load()
+    buf = _c.create_string_buffer(image, len(image) or 1)
+    return int(lib.wsst_read_block(buf, len(image), offset, size))
