@@ -7,6 +7,11 @@
 //      Mask :38-41, Unmask :44-47)
 //   leveldb/util/crc32c.h:11-41     namespace leveldb::crc32c
 //     (Extend :17, Value :20-22, kMaskDelta :24, Mask :29-32, Unmask :35-38)
+//   pebblesdb/src/util/crc32c.h:11-41 the same leveldb::crc32c (one symbol
+//     serves both trees)
+//   rocksdb/util/crc32c.h:14-41     namespace rocksdb::crc32c
+//     (IsFastCrc32Supported :16, Extend :21, Value :23-25, kMaskDelta :27,
+//      Mask :32-35, Unmask :38-41) -- the comparison stores of SURVEY 8f-4
 //
 // Extend/Value keep their reference meaning and stay infallible (host CPU
 // path, crc32c_cpu.cc).  ExtendBatch is new: it hands a whole batch of block
@@ -82,3 +87,22 @@ inline uint32_t Unmask(uint32_t masked_crc) {
 
 }  // namespace crc32c
 }  // namespace leveldb
+
+namespace rocksdb {
+namespace crc32c {
+
+extern std::string IsFastCrc32Supported();
+extern uint32_t Extend(uint32_t init_crc, const char* data, size_t n);
+inline uint32_t Value(const char* data, size_t n) { return Extend(0, data, n); }
+
+static const uint32_t kMaskDelta = 0xa282ead8ul;
+inline uint32_t Mask(uint32_t crc) {
+  return ((crc >> 15) | (crc << 17)) + kMaskDelta;
+}
+inline uint32_t Unmask(uint32_t masked_crc) {
+  uint32_t rot = masked_crc - kMaskDelta;
+  return ((rot >> 17) | (rot << 15));
+}
+
+}  // namespace crc32c
+}  // namespace rocksdb

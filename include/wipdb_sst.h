@@ -64,6 +64,25 @@ int wsst_verify_tables(const char* const* images, const size_t* sizes, size_t n,
                        int bloom_bits, int crc_mode, int device, int* codes,
                        uint64_t* blocks_checked, uint64_t* bad_blocks);
 
+/* kv::log::Writer::AddRecord for n records (concatenated + lengths) into a
+ * fresh log (kv/src/db/log_writer.cc), every header CRC in one batch.
+ * *out_size = image size; WSST_ERR_TOO_SMALL when it exceeds cap. */
+int wsst_log_write(const char* records, const uint32_t* lens, size_t n, int recycle,
+                   uint64_t log_number, int crc_mode, int device, char* out, size_t cap,
+                   uint64_t* out_size);
+
+/* kv::log::Reader::ReadRecord (checksum on, initial offset 0) over nlogs log
+ * images, all record CRCs in one batch (kv/src/db/log_reader.cc).  Records of
+ * all logs go to rec_out / rec_lens / rec_offsets (LastRecordOffset) in order,
+ * nrecs[i] per log; corruption reports to drop_bytes and 64-byte
+ * "Corruption: <reason>" slots of drop_reasons, ndrops[i] per log.
+ * WSST_ERR_TOO_SMALL when a capacity is exceeded. */
+int wsst_log_read(const char* const* images, const size_t* sizes, size_t nlogs, int crc_mode,
+                  int device, char* rec_out, size_t rec_cap, uint32_t* rec_lens,
+                  uint64_t* rec_offsets, size_t max_recs, uint64_t* nrecs,
+                  uint64_t* drop_bytes, char* drop_reasons, size_t max_drops,
+                  uint64_t* ndrops);
+
 #ifdef __cplusplus
 }
 #endif

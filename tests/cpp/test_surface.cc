@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "hip_crc32c_batch.h"
-#include "wipdb/crc32c.h"
+#include "util/crc32c.h"  // include/wipdb_compat: the path kv/leveldb/rocksdb sources use
 
 static int g_fail = 0;
 #define CHECK_EQ(a, b)                                                       \
@@ -57,11 +57,16 @@ static uint32_t KvUnmask(uint32_t c) { return kv::crc32c::Unmask(c); }
 static uint32_t LdbExtend(uint32_t c, const char* d, size_t n) { return leveldb::crc32c::Extend(c, d, n); }
 static uint32_t LdbMask(uint32_t c) { return leveldb::crc32c::Mask(c); }
 static uint32_t LdbUnmask(uint32_t c) { return leveldb::crc32c::Unmask(c); }
+static uint32_t RdbExtend(uint32_t c, const char* d, size_t n) { return rocksdb::crc32c::Extend(c, d, n); }
+static uint32_t RdbMask(uint32_t c) { return rocksdb::crc32c::Mask(c); }
+static uint32_t RdbUnmask(uint32_t c) { return rocksdb::crc32c::Unmask(c); }
 
 int main(int argc, char** argv) {
   const bool expect_gpu = argc > 1 && atoi(argv[1]) != 0;
   StandardResults<KvExtend, KvMask, KvUnmask>();
   StandardResults<LdbExtend, LdbMask, LdbUnmask>();
+  StandardResults<RdbExtend, RdbMask, RdbUnmask>();
+  CHECK_EQ(rocksdb::crc32c::IsFastCrc32Supported() == kv::crc32c::IsFastCrc32Supported(), 1);
   CHECK_EQ(kv::crc32c::Value("hello", 5), leveldb::crc32c::Value("hello", 5));
   CHECK_EQ(kv::crc32c::kMaskDelta, 0xa282ead8u);
 

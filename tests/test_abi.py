@@ -55,6 +55,7 @@ def _build_surface_test(tmp_path):
     exe = str(tmp_path / "test_surface")
     libdir = os.path.join(REPO, "wipdb_amd", "lib")
     cmd = ["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
+           "-I", os.path.join(REPO, "include", "wipdb_compat"),
            os.path.join(REPO, "tests", "cpp", "test_surface.cc"), "-L", libdir,
            "-lhip_crc32c_batch", f"-Wl,-rpath,{libdir}", "-o", exe]
     subprocess.run(cmd, check=True)

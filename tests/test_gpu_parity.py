@@ -231,6 +231,7 @@ def test_cpp_surface_drop_in_gpu(tmp_path):
     exe = str(tmp_path / "test_surface")
     libdir = os.path.join(REPO, "wipdb_amd", "lib")
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
+           "-I", os.path.join(REPO, "include", "wipdb_compat"),
                     os.path.join(REPO, "tests", "cpp", "test_surface.cc"), "-L", libdir,
                     "-lhip_crc32c_batch", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
     r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=300)

@@ -5,7 +5,9 @@
 // cpuid dispatch :1202-1224, here done lazily inside crc32c_cpu.cc, so there
 // is no static-initialisation-order hazard when Extend is called from
 // another translation unit's static constructor).  leveldb::crc32c::Extend
-// replaces leveldb/util/crc32c.cc:275-380.
+// replaces leveldb/util/crc32c.cc:275-380 (and pebblesdb/src/util/crc32c.cc,
+// the same symbol); rocksdb::crc32c::Extend / IsFastCrc32Supported replace
+// rocksdb/util/crc32c.cc's.
 #include <stdint.h>
 
 #include <atomic>
@@ -48,6 +50,18 @@ uint32_t Extend(uint32_t init_crc, const char* data, size_t n) {
 }
 }  // namespace crc32c
 }  // namespace leveldb
+
+namespace rocksdb {
+namespace crc32c {
+std::string IsFastCrc32Supported() {
+  // rocksdb/util/crc32c.cc's wording for the SSE4.2 build
+  return wipdb::cpu::IsAccelerated() ? "Supported on x86" : "Not supported on x86";
+}
+uint32_t Extend(uint32_t init_crc, const char* data, size_t n) {
+  return wipdb::cpu::Extend(init_crc, data, n);
+}
+}  // namespace crc32c
+}  // namespace rocksdb
 
 namespace wipdb {
 namespace crc32c {

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/wipdb/log.h"
 #include "../../include/wipdb/table.h"
 
 namespace {
@@ -116,6 +117,70 @@ int wsst_verify_tables(const char* const* images, const size_t* sizes, size_t n,
   if (blocks_checked) *blocks_checked = checked;
   if (bad_blocks) *bad_blocks = bad;
   return first;
+}
+
+int wsst_log_write(const char* records, const uint32_t* lens, size_t n, int recycle,
+                   uint64_t log_number, int crc_mode, int device, char* out, size_t cap,
+                   uint64_t* out_size) {
+  CrcMode mode;
+  if (!ModeOf(crc_mode, &mode) || !out || !out_size || (n && (!records || !lens)))
+    return WSST_ERR_INVALID;
+  std::vector<std::string_view> recs(n);
+  size_t o = 0;
+  for (size_t i = 0; i < n; ++i) {
+    recs[i] = std::string_view(records + o, lens[i]);
+    o += lens[i];
+  }
+  std::string img;
+  const Status s = wipdb::log::WriteLog(recs, recycle != 0, log_number, mode, device, &img);
+  if (!s.ok()) return Code(s);
+  *out_size = img.size();
+  if (img.size() > cap) return WSST_ERR_TOO_SMALL;
+  memcpy(out, img.data(), img.size());
+  return WSST_OK;
+}
+
+int wsst_log_read(const char* const* images, const size_t* sizes, size_t nlogs, int crc_mode,
+                  int device, char* rec_out, size_t rec_cap, uint32_t* rec_lens,
+                  uint64_t* rec_offsets, size_t max_recs, uint64_t* nrecs,
+                  uint64_t* drop_bytes, char* drop_reasons, size_t max_drops,
+                  uint64_t* ndrops) {
+  CrcMode mode;
+  if (!ModeOf(crc_mode, &mode) || (nlogs && (!images || !sizes || !nrecs || !ndrops)))
+    return WSST_ERR_INVALID;
+  std::vector<std::vector<wipdb::log::Record>> recs;
+  std::vector<std::vector<wipdb::log::Drop>> drops;
+  const Status s = wipdb::log::ReadLogs(images, sizes, nlogs, mode, device, &recs, &drops);
+  if (!s.ok()) return Code(s);
+  size_t r = 0, d = 0, used = 0;
+  int rc = WSST_OK;
+  for (size_t i = 0; i < nlogs; ++i) {
+    nrecs[i] = recs[i].size();
+    ndrops[i] = drops[i].size();
+    for (const auto& x : recs[i]) {
+      if (r >= max_recs || used + x.data.size() > rec_cap || !rec_out || !rec_lens ||
+          !rec_offsets) {
+        rc = WSST_ERR_TOO_SMALL;
+        break;
+      }
+      memcpy(rec_out + used, x.data.data(), x.data.size());
+      rec_lens[r] = static_cast<uint32_t>(x.data.size());
+      rec_offsets[r] = x.offset;
+      used += x.data.size();
+      ++r;
+    }
+    for (const auto& x : drops[i]) {
+      if (d >= max_drops || !drop_bytes || !drop_reasons) {
+        rc = WSST_ERR_TOO_SMALL;
+        break;
+      }
+      drop_bytes[d] = x.bytes;
+      strncpy(drop_reasons + 64 * d, x.reason.c_str(), 63);
+      drop_reasons[64 * d + 63] = 0;
+      ++d;
+    }
+  }
+  return rc;
 }
 
 }  // extern "C"

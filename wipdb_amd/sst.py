@@ -4,6 +4,8 @@ its C-ABI (include/wipdb_sst.h).
     build_tables(tables, ...)   kv::TableBuilder's SST bytes, block CRCs in one batch
     verify_tables(images, ...)  Table::Open(paranoid) + verified iteration, batched
     read_block(image, off, n)   ReadBlock(verify_checksums)
+    log_write(records, ...)     kv::log::Writer::AddRecord bytes, record CRCs in one batch
+    log_read(images, ...)       kv::log::Reader::ReadRecord over whole logs, CRCs batched
 
 Status codes follow wipdb_sst.h: 0 OK, 1 corruption, 2 checksum mismatch,
 3 other; negative = API / device error (raised as SstError).
@@ -34,6 +36,10 @@ _PROTOS = {
     "wsst_read_block": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64]),
     "wsst_verify_tables": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_int, _c.c_int, _vp, _vp,
                                       _vp]),
+    "wsst_log_write": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_uint64, _c.c_int, _c.c_int, _vp,
+                                  _sz, _vp]),
+    "wsst_log_read": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_int, _vp, _sz, _vp, _vp, _sz, _vp,
+                                 _vp, _vp, _sz, _vp]),
 }
 _bound = None
 
@@ -119,3 +125,57 @@ def read_block(image: bytes, offset: int, size: int) -> int:
     lib = _load()
     buf = _c.create_string_buffer(image, len(image) or 1)
     return int(lib.wsst_read_block(buf, len(image), offset, size))
+
+
+def log_write(records: Sequence[bytes], recycle: bool = False, log_number: int = 0,
+              crc_mode: int = CRC_BATCH_AUTO, device: int = 0) -> bytes:
+    lib = _load()
+    blob, lens = _blob(list(records))
+    cap = len(blob) + 11 * (len(records) + len(blob) // 32000 + 2) + 32768
+    out = _c.create_string_buffer(cap)
+    size = _c.c_uint64(0)
+    b = _c.create_string_buffer(blob, len(blob) or 1)
+    rc = lib.wsst_log_write(b, lens.ctypes.data if len(records) else None, len(records),
+                            int(recycle), log_number, crc_mode, device, out, cap, _c.byref(size))
+    if rc != OK:
+        raise SstError(f"wsst_log_write: {rc}")
+    return out.raw[:size.value]
+
+
+def log_read(images: Sequence[bytes], crc_mode: int = CRC_BATCH_AUTO, device: int = 0):
+    """Per log: (records [(LastRecordOffset, bytes)], drops [(bytes, reason)])."""
+    lib = _load()
+    n = len(images)
+    bufs = [_c.create_string_buffer(im, len(im) or 1) for im in images]
+    ptrs = (_c.c_void_p * max(n, 1))(*[_c.addressof(b) for b in bufs])
+    sizes = np.array([len(im) for im in images] or [0], dtype=np.uint64)
+    total = int(sizes.sum())
+    max_recs = total // 7 + 16
+    rec_out = _c.create_string_buffer(total + 16)
+    rec_lens = np.zeros(max_recs, np.uint32)
+    rec_offs = np.zeros(max_recs, np.uint64)
+    nrecs = np.zeros(max(n, 1), np.uint64)
+    max_drops = total // 7 + 16
+    drop_bytes = np.zeros(max_drops, np.uint64)
+    reasons = _c.create_string_buffer(64 * max_drops)
+    ndrops = np.zeros(max(n, 1), np.uint64)
+    rc = lib.wsst_log_read(ptrs, sizes.ctypes.data, n, crc_mode, device, rec_out, total + 16,
+                           rec_lens.ctypes.data, rec_offs.ctypes.data, max_recs,
+                           nrecs.ctypes.data, drop_bytes.ctypes.data, reasons, max_drops,
+                           ndrops.ctypes.data)
+    if rc != OK:
+        raise SstError(f"wsst_log_read: {rc}")
+    raw, rraw = rec_out.raw, reasons.raw
+    out, r, d, used = [], 0, 0, 0
+    for i in range(n):
+        recs, drops = [], []
+        for _ in range(int(nrecs[i])):
+            ln = int(rec_lens[r])
+            recs.append((int(rec_offs[r]), raw[used:used + ln]))
+            used += ln
+            r += 1
+        for _ in range(int(ndrops[i])):
+            drops.append((int(drop_bytes[d]), rraw[64 * d:64 * d + 64].split(b"\0")[0].decode()))
+            d += 1
+        out.append((recs, drops))
+    return out
