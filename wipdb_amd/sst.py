@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import time
 from typing import Sequence
 
 import numpy as np
@@ -42,6 +43,8 @@ _PROTOS = {
                                  _vp, _vp, _sz, _vp]),
 }
 _bound = None
+# wall time of the last native call (the C-ABI call alone, no Python packing)
+last_call_seconds = 0.0
 
 
 class SstError(RuntimeError):
@@ -77,23 +80,39 @@ def build_tables(tables: Sequence[Sequence[tuple[bytes, bytes]]], block_size: in
                  device: int = 0) -> tuple[int, list[bytes], int]:
     """Builds every table (a sorted list of (key, value)) and finishes them
     together.  Returns (status code, table images, blocks CRC'd in batches)."""
-    lib = _load()
-    n = len(tables)
     entries = np.array([len(t) for t in tables], dtype=np.uint64)
     flat = [kv for t in tables for kv in t]
     keys, klen = _blob([k for k, _ in flat])
     vals, vlen = _blob([v for _, v in flat])
-    cap = 2 * (len(keys) + len(vals)) + 4096 * (n + 1) + 64 * len(flat)
+    return build_tables_raw(entries, keys, klen, vals, vlen, block_size, restart_interval,
+                            bloom_bits, max_buffer_size, crc_mode, device)
+
+
+def build_tables_raw(entries, keys: bytes, klen, vals: bytes, vlen, block_size: int = 4096,
+                     restart_interval: int = 16, bloom_bits: int = 0,
+                     max_buffer_size: int = 4 << 20, crc_mode: int = CRC_BATCH_AUTO,
+                     device: int = 0) -> tuple[int, list[bytes], int]:
+    """build_tables over pre-packed blobs: entries[t] pairs for table t, keys
+    and values concatenated with their uint32 lengths."""
+    lib = _load()
+    entries = np.ascontiguousarray(entries, dtype=np.uint64)
+    klen = np.ascontiguousarray(klen, dtype=np.uint32)
+    vlen = np.ascontiguousarray(vlen, dtype=np.uint32)
+    n = entries.size
+    cap = 2 * (len(keys) + len(vals)) + 4096 * (n + 1) + 64 * int(klen.size)
     out = _c.create_string_buffer(cap)
     offs = np.zeros(max(n, 1), np.uint64)
     sizes = np.zeros(max(n, 1), np.uint64)
     batched = _c.c_uint64(0)
     kbuf = _c.create_string_buffer(keys, len(keys) or 1)
     vbuf = _c.create_string_buffer(vals, len(vals) or 1)
+    global last_call_seconds
+    t0 = time.perf_counter()
     rc = lib.wsst_build_tables(n, entries.ctypes.data, kbuf, klen.ctypes.data, vbuf,
                                vlen.ctypes.data, block_size, restart_interval, bloom_bits,
                                max_buffer_size, crc_mode, device, out, cap, offs.ctypes.data,
                                sizes.ctypes.data, _c.byref(batched))
+    last_call_seconds = time.perf_counter() - t0
     if rc < 0:
         raise SstError(f"wsst_build_tables: {rc}")
     raw = out.raw
@@ -111,9 +130,12 @@ def verify_tables(images: Sequence[bytes], bloom_bits: int = 0, crc_mode: int = 
     sizes = np.array([len(im) for im in images] or [0], dtype=np.uint64)
     codes = np.zeros(max(n, 1), np.int32)
     chk, bad = _c.c_uint64(0), _c.c_uint64(0)
+    global last_call_seconds
+    t0 = time.perf_counter()
     rc = lib.wsst_verify_tables(ptrs, sizes.ctypes.data, n, bloom_bits, crc_mode, device,
                                 codes.ctypes.data, _c.byref(chk) if count_blocks else None,
                                 _c.byref(bad) if count_blocks else None)
+    last_call_seconds = time.perf_counter() - t0
     if rc < 0:
         raise SstError(f"wsst_verify_tables: {rc}")
     if count_blocks:
@@ -135,8 +157,11 @@ def log_write(records: Sequence[bytes], recycle: bool = False, log_number: int =
     out = _c.create_string_buffer(cap)
     size = _c.c_uint64(0)
     b = _c.create_string_buffer(blob, len(blob) or 1)
+    global last_call_seconds
+    t0 = time.perf_counter()
     rc = lib.wsst_log_write(b, lens.ctypes.data if len(records) else None, len(records),
                             int(recycle), log_number, crc_mode, device, out, cap, _c.byref(size))
+    last_call_seconds = time.perf_counter() - t0
     if rc != OK:
         raise SstError(f"wsst_log_write: {rc}")
     return out.raw[:size.value]
@@ -159,10 +184,13 @@ def log_read(images: Sequence[bytes], crc_mode: int = CRC_BATCH_AUTO, device: in
     drop_bytes = np.zeros(max_drops, np.uint64)
     reasons = _c.create_string_buffer(64 * max_drops)
     ndrops = np.zeros(max(n, 1), np.uint64)
+    global last_call_seconds
+    t0 = time.perf_counter()
     rc = lib.wsst_log_read(ptrs, sizes.ctypes.data, n, crc_mode, device, rec_out, total + 16,
                            rec_lens.ctypes.data, rec_offs.ctypes.data, max_recs,
                            nrecs.ctypes.data, drop_bytes.ctypes.data, reasons, max_drops,
                            ndrops.ctypes.data)
+    last_call_seconds = time.perf_counter() - t0
     if rc != OK:
         raise SstError(f"wsst_log_read: {rc}")
     raw, rraw = rec_out.raw, reasons.raw
