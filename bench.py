@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--stride", type=int, default=BLOCK,
                    help="diagnostic: block stride (0 = every block reads the same 4 KiB, "
                         "i.e. cache-resident compute ceiling); the headline uses 4096")
+    p.add_argument("--fill", choices=["splitmix", "zero"], default="splitmix",
+                   help="diagnostic: block contents (zero = low-toggle data, to probe "
+                        "the power/clock limit); the headline uses splitmix")
     p.add_argument("--order", choices=["natural", "group", "cu"], default="natural",
                    help="diagnostic: which block each descriptor names (natural: block i; "
                         "group: every lane group sweeps its own contiguous run; cu: every "
@@ -157,7 +160,11 @@ def main():
     first, nblk = block_shard(rank, world, a.blocks)  # weak scaling, no collective
     data = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    eng.fill_splitmix64_device(data, SEED, first_word=first * BLOCK // 8, stream=stream.cuda_stream)
+    if a.fill == "zero":
+        data.zero_()
+    else:
+        eng.fill_splitmix64_device(data, SEED, first_word=first * BLOCK // 8,
+                                   stream=stream.cuda_stream)
     idx = torch.arange(nblk, dtype=torch.int64, device=dev)
     if a.order != "natural":
         # span s is taken by lane group q = s % G at step k = s // G of the
@@ -251,13 +258,16 @@ def main():
         }
         if rs:
             line["readstream_ceiling"] = rs
+        if a.fill != "splitmix":
+            line["config"]["diagnostic_fill"] = a.fill
+            line["metric"] += " [DIAGNOSTIC fill]"
         if a.order != "natural":
             line["config"]["diagnostic_order"] = a.order
             line["metric"] += " [DIAGNOSTIC order]"
         if a.stride != BLOCK:
             line["config"]["diagnostic_stride"] = a.stride
             line["metric"] += " [DIAGNOSTIC stride, not the headline]"
-        if world == 1 and not a.no_cpu_baseline and a.stride == BLOCK:
+        if world == 1 and not a.no_cpu_baseline and a.stride == BLOCK and a.fill == "splitmix":
             gpu_crc = out.cpu().numpy().view(np.uint32)
             cb, par = cpu_baseline(SEED, gpu_crc, first, a.cpu_seconds)
             line["cpu_baseline"] = cb

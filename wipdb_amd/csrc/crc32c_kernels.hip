@@ -410,8 +410,15 @@ __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, con
     pad_g[g] = live ? kSegChunks - (hn >> 4) : 0u;
     base_g[g] = live ? (s[g].start & ~uint64_t(15)) : reinterpret_cast<uint64_t>(dummy);
   }
-  const bool hi = lane >= static_cast<uint32_t>(G);
-  const uint32_t gl = lane & (G - 1);
+  // an opaque lane copy: the per-load chunk indices derived from it are
+  // recomputed here (one VALU each) rather than hoisted out of the wave loop
+  // into registers that the ring needs
+  uint32_t ln = lane;
+#if WIPDB_OPAQUE_LANE
+  asm volatile("" : "+v"(ln));
+#endif
+  const bool hi = ln >= static_cast<uint32_t>(G);
+  const uint32_t gl = ln & (G - 1);
   const uint32_t pad = gsel(hi, pad_g[0], pad_g[1]);
   g_u32x4* b = reinterpret_cast<g_u32x4*>(gsel(hi, base_g[0], base_g[1]));
 #if WIPDB_LEAN_ISSUE
