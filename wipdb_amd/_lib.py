@@ -54,6 +54,8 @@ _PROTOS = {
         _c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _vp, _vp, _vp, _vp, _vp, _sz, _c.c_int]),
     "hcrc_host_alloc": (_c.c_int, [_sz, _c.POINTER(_vp)]),
     "hcrc_host_free": (_c.c_int, [_vp]),
+    "hcrc_host_register": (_c.c_int, [_vp, _sz]),
+    "hcrc_host_unregister": (_c.c_int, [_vp]),
     "hcrc_readstream_async": (_c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint32, _vp, _sz, _vp]),
     "hcrc_fill_splitmix64_async": (
         _c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint64, _c.c_uint64, _vp]),
