@@ -252,8 +252,9 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) {
 
 // ---------------------------------------------------------------------------
 // Segments.  A span is cut at 4 KiB boundaries of its 16-byte chunk grid:
-// segment = [start, start+n) with n = min(rest, 4096 - (start & 15)), so its
-// main region holds at most 256 chunks = one chunk per chain of its group.
+// segment = [start, start+n) with n = rest if rest <= 4111 - (start & 15),
+// else 4096 - (start & 15), so its main region holds at most 256 chunks and
+// its ragged tail fewer than 16 bytes.
 // Geometry is kept in 32-bit offsets from the 16-byte aligned base:
 // hn = (start & 15) + n; the main region is chunks [0, hn >> 4), the ragged
 // tail hn & 15 bytes after it.  All fields are uniform.
@@ -361,8 +362,12 @@ struct SegCursor {
     // another slot's value at the ring's merge points)
     Slot sl{0, 0, 0, 0};
     if (left == 0u) return sl;
+    // a segment is at most 256 chunks of the 16-byte grid; when the rest of
+    // the span fits that plus a ragged tail (< 16 bytes, fed after the
+    // fold), it is the last segment -- so an unaligned 4 KiB block is one
+    // segment, not 4096 - h bytes and an h-byte second one
     const uint32_t room = 4096u - static_cast<uint32_t>(start & 15u);
-    const bool last = rest <= room;
+    const bool last = rest <= room + 15u;
     const uint32_t n = last ? rest : room;
     sl.start = start;
     sl.init = init;
