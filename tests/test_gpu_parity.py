@@ -278,3 +278,55 @@ def test_cpp_surface_drop_in_gpu(tmp_path):
                     "-lhip_crc32c_batch", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
     r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_concurrent_host_batches_share_a_context(engine, oracle):
+    """Reentrancy (flush, compaction and reader threads call the
+    CRC concurrently): 8 host threads drive hcrc_batch on one context, and 4
+    more the device-resident entry point on their own streams, at once;
+    every result equals the oracle."""
+    import threading
+
+    import torch
+    rng = np.random.default_rng(77)
+    bufs, want, dev = [], [], []
+    for t in range(8):
+        b = rng.integers(0, 256, size=(1 << 20) + 4096, dtype=np.uint8)
+        lens = rng.integers(0, 9000, size=300).astype(np.uint32)
+        offs = np.array([int(rng.integers(0, b.size - int(x))) for x in lens], np.uint64)
+        bufs.append((b, offs, lens))
+        want.append(oracle.batch(b, offs, lens))
+    for t in range(4):
+        b, offs, lens = bufs[t]
+        dev.append((torch.from_numpy(b).cuda(), torch.from_numpy(offs.view(np.int64)).cuda(),
+                    torch.from_numpy(lens.view(np.int32)).cuda(), torch.cuda.Stream()))
+    got, errs = [None] * 12, []
+
+    def host(i):
+        try:
+            for _ in range(5):
+                got[i] = engine.batch(*bufs[i])
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    def device(i):
+        try:
+            b, o, ln, st = dev[i]
+            for _ in range(5):
+                out = engine.batch_device(b, o, ln, stream=st)
+            st.synchronize()
+            got[8 + i] = out.cpu().numpy().view(np.uint32)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=host, args=(i,)) for i in range(8)]
+    th += [threading.Thread(target=device, args=(i,)) for i in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errs, errs
+    for i in range(8):
+        np.testing.assert_array_equal(got[i], want[i])
+    for i in range(4):
+        np.testing.assert_array_equal(got[8 + i], want[i])

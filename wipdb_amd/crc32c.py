@@ -142,6 +142,8 @@ class Engine:
         if stream is None:
             import torch
             return int(torch.cuda.current_stream().cuda_stream)
+        if hasattr(stream, "cuda_stream"):  # a torch.cuda.Stream
+            return int(stream.cuda_stream)
         return int(stream)
 
     def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
