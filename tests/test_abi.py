@@ -44,6 +44,14 @@ def test_invalid_arguments_are_rejected_without_device():
     assert (rc == 0 and n.value >= 0) or (rc == _lib.HCRC_ERR_NO_DEVICE and n.value == 0)
 
 
+def test_host_memory_entry_points_validate_arguments():
+    lib = _lib.load()
+    assert lib.hcrc_host_register(None, 4096) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_host_register(1, 0) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_host_unregister(None) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_host_alloc(16, None) == _lib.HCRC_ERR_INVALID
+
+
 def test_ctx_create_bad_device_index():
     lib = _lib.load()
     ctx = ctypes.c_void_p()

@@ -604,7 +604,8 @@ int hcrc_batch_multi(const int* devices, int ndev, const void* base,
 
 int hcrc_host_alloc(size_t bytes, void** out_ptr) {
   if (!out_ptr) return HCRC_ERR_INVALID;
-  HCRC_CHECK(hipHostMalloc(out_ptr, bytes));
+  // portable + mapped: every device of a multi-GPU batch reads it zero-copy
+  HCRC_CHECK(hipHostMalloc(out_ptr, bytes, hipHostMallocPortable | hipHostMallocMapped));
   return HCRC_OK;
 }
 
