@@ -70,6 +70,12 @@ extern "C" {
 #define HCRC_HOST_PTRS 0x0    /* all array/data pointers are host memory    */
 #define HCRC_DEVICE_PTRS 0x1  /* all array/data pointers are device memory  */
 #define HCRC_MASK_OUTPUT 0x2  /* write Mask(crc) instead of crc             */
+/* Spans of at most 1024 bytes are checksummed by the small-span kernel
+ * (8 per wave slot) instead of a whole 4 KiB group segment each: a partition
+ * pass compacts them, stream-ordered scratch (hipMallocAsync).  Same
+ * results; pays off for batches with many short spans (WAL records, small
+ * meta blocks).  hcrc_batch on host memory chooses it by itself. */
+#define HCRC_SPLIT_SMALL 0x4
 
 typedef struct hcrc_ctx hcrc_ctx;
 

@@ -72,6 +72,9 @@ def check_sample(host, offs, lens, got, rng, k=4000):
     return int((want != got[idx]).sum())
 
 
+SPLIT = False  # --split: HCRC_SPLIT_SMALL on the device batches
+
+
 def run_mixed(eng, d, stream, rng, gib):
     nbytes = int(gib * 2**30)
     host = rng.integers(0, 256, nbytes, dtype=np.uint8)
@@ -80,7 +83,8 @@ def run_mixed(eng, d, stream, rng, gib):
     offs, lens, L = zipf_spans(rng, nbytes, BUCKETS)
     do, dl = dev(offs, d), dev(lens, d)
     out = torch.empty(offs.size, dtype=torch.int32, device=d)
-    t = time_kernel(lambda: eng.batch_device(dbuf, do, dl, None, out, stream=stream.cuda_stream),
+    t = time_kernel(lambda: eng.batch_device(dbuf, do, dl, None, out, stream=stream.cuda_stream,
+                                                 split_small=SPLIT),
                     stream, 10)
     got = out.cpu().numpy().view(np.uint32)
     res["mixed"] = {"spans": int(offs.size), "bytes": int(lens.sum()),
@@ -91,7 +95,8 @@ def run_mixed(eng, d, stream, rng, gib):
         dob, dlb = dev(ob, d), dev(lb, d)
         outb = torch.empty(ob.size, dtype=torch.int32, device=d)
         tb = time_kernel(lambda: eng.batch_device(dbuf, dob, dlb, None, outb,
-                                                  stream=stream.cuda_stream), stream, 10)
+                                                  stream=stream.cuda_stream, split_small=SPLIT),
+                         stream, 10)
         gotb = outb.cpu().numpy().view(np.uint32)
         res["buckets"][str(b)] = {"spans": int(ob.size),
                                   "GiBps": round(float(lb.sum()) / tb / 2**30, 1),
@@ -107,7 +112,7 @@ def run_mixed(eng, d, stream, rng, gib):
         o_i, l_i = do[lo:lo + per], dl[lo:lo + per]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream)
+        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream, split_small=SPLIT)
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t0)
     lat = np.array(lat[20:]) * 1e6
@@ -172,10 +177,13 @@ def run_host4k(eng, rng, nblk):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="mixed,sst,host4k")
+    ap.add_argument("--split", action="store_true", help="HCRC_SPLIT_SMALL on device batches")
     ap.add_argument("--mixed-gib", type=float, default=2.0)
     ap.add_argument("--ssts", type=int, default=256)
     ap.add_argument("--host-blocks", type=int, default=1 << 18)
     a = ap.parse_args()
+    global SPLIT
+    SPLIT = a.split
     rng = np.random.default_rng(42)
     d = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(d)

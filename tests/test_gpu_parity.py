@@ -34,11 +34,11 @@ def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
 
-def _run_device(engine, buf, offs, lens, inits=None, mask=False):
+def _run_device(engine, buf, offs, lens, inits=None, mask=False, split=False):
     out = engine.batch_device(_t(buf), _t(np.asarray(offs, np.uint64)),
                               _t(np.asarray(lens, np.uint32)),
                               None if inits is None else _t(np.asarray(inits, np.uint32)),
-                              mask_output=mask)
+                              mask_output=mask, split_small=split)
     return _u32(out)
 
 
@@ -132,7 +132,30 @@ def test_small_spans_exhaustive(engine, oracle):
     offs, lens, inits = (np.array(offs, np.uint64), np.array(lens, np.uint32),
                          np.array(inits, np.uint32))
     got = _run_device(engine, buf, offs, lens, inits)
-    np.testing.assert_array_equal(got, oracle.batch(buf, offs, lens, inits))
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(got, want)
+    # the same on the small-span kernel (HCRC_SPLIT_SMALL): every length
+    # 0..300 at 48 offsets, with and without inits, masked too
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits, split=True), want)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits, mask=True, split=True),
+                                  np.array([oracle.lib.oracle_mask(int(x)) for x in want], np.uint32))
+
+
+def test_split_small_boundaries_and_mix(engine, oracle):
+    """The small/large cut (1024 B) at every alignment, interleaved with
+    large spans, on the split path -- each span goes to exactly one kernel."""
+    rng = np.random.default_rng(21)
+    buf = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    lens = []
+    for n in list(range(1000, 1050)) + [1, 15, 16, 17, 500, 4096, 4111, 4112, 8191, 70000]:
+        lens += [n] * 20
+    lens = np.array(rng.permutation(lens), np.uint32)
+    offs = np.array([int(rng.integers(0, buf.size - 70001)) for _ in lens], np.uint64)
+    inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits, split=True), want)
+    # host path: chooses the split by itself (>= 256 small spans)
+    np.testing.assert_array_equal(engine.batch(buf, offs, lens, inits), want)
 
 
 def test_segment_and_large_spans(engine, oracle):
@@ -168,7 +191,9 @@ def test_zipf_mixed_sst_packing(engine, oracle):
         cur += n + 5
     offs, lens = np.array(offs, np.uint64), np.array(lens, np.uint32)
     got = _run_device(engine, buf, offs, lens)
-    np.testing.assert_array_equal(got, oracle.batch(buf, offs, lens))
+    want = oracle.batch(buf, offs, lens)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, split=True), want)
 
 
 def test_full_size_4k_blocks(engine, oracle, reference):

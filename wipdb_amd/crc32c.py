@@ -19,7 +19,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HcrcError, check
+from ._lib import HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HCRC_SPLIT_SMALL, HcrcError, check
 
 MASK_DELTA = 0xA282EAD8
 
@@ -147,14 +147,18 @@ class Engine:
         return int(stream)
 
     def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
-                     mask_output: bool = False, stream=None):
+                     mask_output: bool = False, stream=None, split_small: bool = False):
         """Asynchronous batch on device tensors; returns the uint32 out tensor
-        (int32 storage).  Enqueued on ``stream`` (default: torch's current)."""
+        (int32 storage).  Enqueued on ``stream`` (default: torch's current).
+        ``split_small``: HCRC_SPLIT_SMALL (spans <= 1 KiB on the small-span
+        kernel)."""
         import torch
         n = int(offsets_t.numel())
         if out_t is None:
             out_t = torch.empty(n, dtype=torch.int32, device=base_t.device)
         flags = HCRC_DEVICE_PTRS | (HCRC_MASK_OUTPUT if mask_output else 0)
+        if split_small:
+            flags |= HCRC_SPLIT_SMALL
         check(self._lib.hcrc_batch_async(self._ctx, _ptr(base_t), _ptr(offsets_t), _ptr(lengths_t),
                                          _ptr(inits_t), _ptr(out_t), n, flags,
                                          self._stream_of(stream)), "hcrc_batch_async")

@@ -13,6 +13,21 @@ namespace dev {
 constexpr int kWaves = WIPDB_WAVES;      // waves per workgroup (1 WG per CU)
 constexpr int kThreads = kWaves * 64;    // 1024 threads
 constexpr uint32_t kFlagMask = 0x2;      // == HCRC_MASK_OUTPUT
+// spans kernel: leave spans of at most kSmallMax bytes to the small-span
+// kernel (HCRC_SPLIT_SMALL, crc32c_small.inc)
+constexpr uint32_t kFlagSkipSmall = 0x4;
+constexpr uint32_t kSmallMax = 1024;
+
+// Compacted descriptors of a batch's small spans (written by
+// crc32c_partition_kernel, read by crc32c_small_kernel); count is a
+// device counter.
+struct SmallList {
+  uint64_t* off;
+  uint32_t* len;
+  uint32_t* init;
+  uint32_t* id;  // the span's index in the batch (its output slot)
+  uint32_t* count;
+};
 
 // Spans in flight per wave: the wave is split into kGroups lane groups of
 // kGroupLanes lanes; each group CRCs its own span, kChunksPerLane 16-byte

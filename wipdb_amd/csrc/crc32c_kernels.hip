@@ -344,9 +344,22 @@ struct SegCursor {
   uint64_t start;
   uint32_t rest, init, first, left;  // left: spans not yet finished, incl. this one
   uint32_t ord;                      // ordinal of the current span
+  bool skip;                         // kFlagSkipSmall: small spans are the small kernel's
+
+  // With `skip`, step over spans of at most kSmallMax bytes (their ordinals
+  // still count, so output slots stay put).
+  __device__ __forceinline__ void skip_small(Src& src, int g, uint64_t s0, uint64_t stride,
+                                            uint32_t lane) {
+    while (skip && left != 0u && rest <= kSmallMax) {
+      ++ord;
+      --left;
+      if (left != 0u) src.desc(g, s0 + static_cast<uint64_t>(ord) * stride, stride, lane, start,
+                               rest, init);
+    }
+  }
 
   __device__ __forceinline__ void begin(Src& src, int g, uint64_t s, uint64_t stride,
-                                       uint32_t lane) {
+                                       uint32_t lane, bool skip_small_spans) {
     // s < stride always, so this is ceil((count - s) / stride) or 0 -- no compare
     left = static_cast<uint32_t>((src.count + stride - 1 - s) / stride);
     first = 1u;
@@ -354,7 +367,9 @@ struct SegCursor {
     start = 0;
     rest = 0;
     init = 0;
+    skip = skip_small_spans;
     if (left != 0u) src.desc(g, s, stride, lane, start, rest, init);
+    skip_small(src, g, s, stride, lane);
   }
   __device__ __forceinline__ Slot next(Src& src, int g, uint64_t s0, uint64_t stride,
                                        uint32_t lane) {
@@ -379,6 +394,7 @@ struct SegCursor {
       --left;
       if (left != 0u) src.desc(g, s0 + static_cast<uint64_t>(ord) * stride, stride, lane, start,
                                rest, init);
+      skip_small(src, g, s0, stride, lane);
     } else {
       start += n;
       rest -= n;
@@ -656,7 +672,7 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], 
 // and crc uniform).
 template <typename Src, typename Emit>
 __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t waves,
-                                          const void* dummy, Emit emit) {
+                                          const void* dummy, bool skip_small, Emit emit) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l4 = (threadIdx.x & 31u) * 4u;
   const uint32_t s0 = l4 | ((l4 | 0x80u) << 8) | (1u << 24);
@@ -668,7 +684,7 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
   uint32_t live = 0;  // groups with spans left (checked once: all zero -> return)
 #pragma unroll
   for (int g = 0; g < S; ++g) {
-    cur[g].begin(src, g, wave * S + g, stride, lane);
+    cur[g].begin(src, g, wave * S + g, stride, lane, skip_small);
     chain[g] = 0;
     live |= cur[g].left;
   }
@@ -795,7 +811,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
   load_tables(lds, tab);
   DescSource src{base, offsets, lengths, inits, count, 0u, 0, 0, 0, {0, 0}};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, [&](uint64_t span, uint32_t crc, int g) {
+  const bool skip = (flags & kFlagSkipSmall) != 0;
+  run_waves(src, wave_id(), grid_waves(), tab, skip, [&](uint64_t span, uint32_t crc, int g) {
     if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
 }
@@ -809,7 +826,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
   load_tables(lds, tab);
   StridedSource src{base, stride_bytes, length, init, count};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, [&](uint64_t span, uint32_t crc, int g) {
+  run_waves(src, wave_id(), grid_waves(), tab, false, [&](uint64_t span, uint32_t crc, int g) {
     if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
 }
@@ -823,7 +840,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
   DescSource src{base, offsets, lengths, nullptr, count, 1u, 0, 0, 0, {0, 0}};
-  run_waves(src, wave_id(), grid_waves(), tab, [&](uint64_t s, uint32_t crc, int g) {
+  run_waves(src, wave_id(), grid_waves(), tab, false, [&](uint64_t s, uint32_t crc, int g) {
     if (group_leader(g)) {
       const uint8_t* t = base + offsets[s] + lengths[s] + 1;
       const uint32_t stored = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) |
@@ -833,6 +850,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
     }
   });
 }
+
+#include "crc32c_small.inc"
 
 // Read-stream ceiling: the same 16-byte nontemporal loads over fixed-size
 // blocks, XOR-reduced (diagnostic; the roofline's measured denominator).

@@ -42,6 +42,10 @@ __global__ void crc32c_verify_kernel(const uint8_t*, const uint64_t*,
 __global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*,
                                   uint64_t);
 __global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
+__global__ void crc32c_partition_kernel(const uint64_t*, const uint32_t*, const uint32_t*,
+                                        uint64_t, SmallList);
+__global__ void crc32c_small_kernel(const uint8_t*, SmallList, uint32_t*, uint32_t,
+                                    const DevTables*);
 }  // namespace dev
 }  // namespace wipdb
 
@@ -117,16 +121,71 @@ int LaunchGrid(hcrc_ctx* ctx, size_t count) {
   return static_cast<int>(std::max<size_t>(g, 1));
 }
 
+int LaunchSpansKernel(hcrc_ctx* ctx, const void* base, const uint64_t* off,
+                      const uint32_t* len, const uint32_t* init, uint32_t* out,
+                      size_t count, uint32_t kflags, hipStream_t st) {
+  hipLaunchKernelGGL(wipdb::dev::crc32c_spans_kernel, dim3(LaunchGrid(ctx, count)),
+                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+                     static_cast<const uint8_t*>(base), off, len, init, out,
+                     static_cast<uint64_t>(count), kflags, ctx->d_tab);
+  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+}
+
+// HCRC_SPLIT_SMALL: the spans of at most kSmallMax bytes are compacted by
+// the partition kernel and checksummed 8 per wave slot by the small kernel;
+// the spans kernel skips them.  Everything is ordered on `st`, the scratch
+// is stream-ordered (hipMallocAsync / hipFreeAsync), so concurrent calls on
+// different streams never share it.
+int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
+                const uint32_t* init, uint32_t* out, size_t count, uint32_t mask,
+                hipStream_t st) {
+  const size_t n = count;
+  uint8_t* scratch = nullptr;
+  HCRC_CHECK(hipMallocAsync(reinterpret_cast<void**>(&scratch), n * 20 + 64, st));
+  wipdb::dev::SmallList sl;
+  sl.off = reinterpret_cast<uint64_t*>(scratch);
+  sl.len = reinterpret_cast<uint32_t*>(scratch + n * 8);
+  sl.init = sl.len + n;
+  sl.id = sl.init + n;
+  sl.count = sl.id + n;
+  int rc = HCRC_OK;
+  if (hipMemsetAsync(sl.count, 0, 4, st) != hipSuccess) rc = HCRC_ERR_HIP;
+  if (rc == HCRC_OK) {
+    const int pgrid = static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8));
+    hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st, off,
+                       len, init, static_cast<uint64_t>(n), sl);
+    hipLaunchKernelGGL(wipdb::dev::crc32c_small_kernel, dim3(ctx->num_cu),
+                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+                       static_cast<const uint8_t*>(base), sl, out, mask, ctx->d_tab);
+    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+  }
+  if (rc == HCRC_OK)
+    rc = LaunchSpansKernel(ctx, base, off, len, init, out, count,
+                           mask | wipdb::dev::kFlagSkipSmall, st);
+  if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
+  return rc;
+}
+
+// split: HCRC_SPLIT_SMALL requested (device batches) or chosen for a host
+// piece with enough small spans.
 int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off,
                 const uint32_t* len, const uint32_t* init, uint32_t* out,
                 size_t count, int flags, hipStream_t st) {
   if (count == 0) return HCRC_OK;
-  hipLaunchKernelGGL(wipdb::dev::crc32c_spans_kernel, dim3(LaunchGrid(ctx, count)),
-                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
-                     static_cast<const uint8_t*>(base), off, len, init, out,
-                     static_cast<uint64_t>(count),
-                     static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_tab);
-  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+  const uint32_t mask = static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT);
+  if ((flags & HCRC_SPLIT_SMALL) && count < (size_t(1) << 32))
+    return LaunchSplit(ctx, base, off, len, init, out, count, mask, st);
+  return LaunchSpansKernel(ctx, base, off, len, init, out, count, mask, st);
+}
+
+// Host pieces: split when enough spans are small for the small kernel to
+// pay for its two extra launches.
+constexpr size_t kAutoSplitMin = 256;
+
+int AutoSplit(const uint32_t* lengths, size_t n) {
+  size_t small = 0;
+  for (size_t i = 0; i < n && small < kAutoSplitMin; ++i) small += lengths[i] <= wipdb::dev::kSmallMax;
+  return small >= kAutoSplitMin ? HCRC_SPLIT_SMALL : 0;
 }
 
 // Async entry points take the caller's stream; NULL is the HIP default
@@ -262,7 +321,8 @@ int BatchZeroCopy(hcrc_ctx* ctx, const uint8_t* dev_base, const uint64_t* offset
     HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, ctx->stream));
     HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, ctx->stream));
     HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, ctx->stream));
-    rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, s.d_init, s.d_out, n, flags, ctx->stream);
+    rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, s.d_init, s.d_out, n,
+                     flags | AutoSplit(lengths + i, n), ctx->stream);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, ctx->stream));
     HCRC_CHECK(hipEventRecord(s.done, ctx->stream));
@@ -320,7 +380,7 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice,
                               ctx->stream));
     rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, s.d_init, s.d_out, n,
-                     flags, ctx->stream);
+                     flags | AutoSplit(lengths + i, n), ctx->stream);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost,
                               ctx->stream));
@@ -410,6 +470,9 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
   HCRC_CHECK(hipFuncSetAttribute(
       reinterpret_cast<const void*>(wipdb::dev::crc32c_verify_kernel),
       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::dev::crc32c_small_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   std::unique_ptr<DevTables> ht(new DevTables);
   BuildDevTables(ht.get());
   HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_tab), sizeof(DevTables)));
@@ -456,7 +519,7 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets,
                uint32_t* out_crcs, size_t count, int flags) {
   if (!ctx || (count && (!base || !offsets || !lengths || !out_crcs)))
     return HCRC_ERR_INVALID;
-  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT)) return HCRC_ERR_INVALID;
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL)) return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HCRC_CHECK(hipSetDevice(ctx->device));
@@ -477,7 +540,7 @@ int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offset
                      uint32_t* d_out_crcs, size_t count, int flags,
                      void* stream) {
   if (!ctx || !(flags & HCRC_DEVICE_PTRS)) return HCRC_ERR_INVALID;
-  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT)) return HCRC_ERR_INVALID;
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL)) return HCRC_ERR_INVALID;
   if (count && (!d_base || !d_offsets || !d_lengths || !d_out_crcs))
     return HCRC_ERR_INVALID;
   std::lock_guard<std::mutex> lk(ctx->mu);
