@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--stride", type=int, default=BLOCK,
                    help="diagnostic: block stride (0 = every block reads the same 4 KiB, "
                         "i.e. cache-resident compute ceiling); the headline uses 4096")
+    p.add_argument("--len", type=int, default=BLOCK, choices=range(0, 65537), metavar="0..65536",
+                   help="diagnostic: bytes CRC'd per block (<= stride; e.g. 4092 = a 4 KiB "
+                        "on-disk block minus its 5-byte trailer, plus the type byte)")
     p.add_argument("--fill", choices=["splitmix", "zero"], default="splitmix",
                    help="diagnostic: block contents (zero = low-toggle data, to probe "
                         "the power/clock limit); the headline uses splitmix")
@@ -158,7 +161,10 @@ def main():
 
     eng = Engine(local)
     first, nblk = block_shard(rank, world, a.blocks)  # weak scaling, no collective
-    data = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
+    # diagnostic spans longer than the 4 KiB pitch (--len > 4096) run past the
+    # last block: give them slack so every span stays inside the allocation
+    slack = (max(0, a.len - BLOCK) + 4095) // 4096 * 4096
+    data = torch.empty(nblk * BLOCK + slack, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     if a.fill == "zero":
         data.zero_()
@@ -178,7 +184,7 @@ def main():
             per_wg = 2 * 16  # groups per workgroup
             idx = (q // per_wg) * (nblk // (G // per_wg)) + k * per_wg + q % per_wg
     offs = idx * a.stride
-    lens = torch.full((nblk,), BLOCK, dtype=torch.int32, device=dev)
+    lens = torch.full((nblk,), a.len, dtype=torch.int32, device=dev)
     out = torch.empty(nblk, dtype=torch.int32, device=dev)
 
     def step():
@@ -258,6 +264,9 @@ def main():
         }
         if rs:
             line["readstream_ceiling"] = rs
+        if a.len != BLOCK:
+            line["config"]["diagnostic_len"] = a.len
+            line["metric"] += " [DIAGNOSTIC len]"
         if a.fill != "splitmix":
             line["config"]["diagnostic_fill"] = a.fill
             line["metric"] += " [DIAGNOSTIC fill]"
@@ -267,7 +276,8 @@ def main():
         if a.stride != BLOCK:
             line["config"]["diagnostic_stride"] = a.stride
             line["metric"] += " [DIAGNOSTIC stride, not the headline]"
-        if world == 1 and not a.no_cpu_baseline and a.stride == BLOCK and a.fill == "splitmix":
+        if (world == 1 and not a.no_cpu_baseline and a.stride == BLOCK and a.fill == "splitmix"
+                and a.len == BLOCK):
             gpu_crc = out.cpu().numpy().view(np.uint32)
             cb, par = cpu_baseline(SEED, gpu_crc, first, a.cpu_seconds)
             line["cpu_baseline"] = cb

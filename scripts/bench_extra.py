@@ -122,6 +122,31 @@ def run_mixed(eng, d, stream, rng, gib):
     return res
 
 
+def run_verify(eng, d, stream, rng, nblk=1 << 20):
+    """Read side, device-resident (hcrc_verify_async, ReadBlock's check):
+    1 M blocks of 4096 bytes on disk = 4091 contents + type byte + masked
+    crc, every trailer stamped with the right crc, a few corrupted."""
+    B, n = 4096, 4091
+    data = torch.empty(nblk * B, dtype=torch.uint8, device=d)
+    eng.fill_splitmix64_device(data, 7, stream=stream.cuda_stream)
+    offs = torch.arange(nblk, dtype=torch.int64, device=d) * B
+    lens = torch.full((nblk,), n + 1, dtype=torch.int32, device=d)
+    crc = eng.batch_device(data, offs, lens, mask_output=True, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    trailer = data.view(nblk, B)[:, n + 1:n + 5]
+    trailer.copy_(crc.view(torch.uint8).view(nblk, 4))
+    bad = torch.from_numpy(rng.choice(nblk, 64, replace=False)).to(d)
+    data.view(nblk, B)[bad, 100] ^= 1
+    hl = torch.full((nblk,), n, dtype=torch.int32, device=d)
+    st = torch.empty(nblk, dtype=torch.uint8, device=d)
+    t = time_kernel(lambda: eng.verify_device(data, offs, hl, st, stream=stream.cuda_stream),
+                    stream, 10)
+    flagged = int((st == 0).sum())
+    return {"config": "read side: ReadBlock verify of 1 M x 4 KiB device-resident blocks",
+            "blocks": nblk, "GiBps": round(nblk * (n + 1) / t / 2**30, 1),
+            "kernel_ms": round(t * 1e3, 4), "corrupted": 64, "flagged": flagged}
+
+
 def sst_layout(rng, n_sst):
     """8Binsert-shaped SSTs (test_bench/8Binsert.sh): spans cover contents +
     type byte; every block is followed by its 4-byte crc slot."""
@@ -191,6 +216,8 @@ def main():
         for w in a.what.split(","):
             if w == "mixed":
                 r = run_mixed(eng, d, stream, rng, a.mixed_gib)
+            elif w == "verify":
+                r = run_verify(eng, d, stream, rng)
             elif w == "sst":
                 r = run_sst(eng, rng, a.ssts)
             elif w == "host4k":

@@ -95,6 +95,9 @@ constexpr int NL = kChunksPerLane; // 16-byte loads per lane per segment (8)
 constexpr int C = WIPDB_CPC;       // consecutive chunks per chain
 constexpr int K = NL / C;          // chains per lane
 constexpr int S = kGroups;         // groups (spans) per wave (2)
+// A ring slot holds the NL chunk loads plus the group's ragged-tail chunk
+// (d[NL]), loaded with the slot so the tail never waits on memory.
+constexpr int NLT = NL + 1;
 constexpr uint32_t kLogC = C == 1 ? 0 : (C == 2 ? 1 : 2);
 static_assert(G * NL == 256 && S * G == 64 && K * C == NL, "a group segment is 256 chunks");
 static_assert(C == 1 || C == 2 || C == 4, "chunks per chain");
@@ -153,8 +156,9 @@ __device__ __forceinline__ uint32_t feed_word(uint32_t s0, uint32_t r, uint32_t 
 // so their lookups are in flight together).  Chain k's chunks are
 // d[k*C .. k*C + C).
 // WIPDB_ILP chains at a time (fewer: fewer registers hold lookup results).
-template <int SUB>
-__device__ __forceinline__ void feed_chunks(uint32_t s0, uint32_t (&r)[K], const u32x4 (&d)[NL]) {
+template <int SUB, int N>
+__device__ __forceinline__ void feed_chunks(uint32_t s0, uint32_t (&r)[K], const u32x4 (&d)[N]) {
+  static_assert(N >= NL, "a slot holds NL chunks");
   constexpr int I = WIPDB_ILP < K ? WIPDB_ILP : K;
 #pragma unroll
   for (int k0 = 0; k0 < K; k0 += I) {
@@ -285,6 +289,8 @@ struct DescSource {
   const uint32_t* inits;
   uint64_t count;
   uint32_t extra;  // bytes added to every length (verify: +1 type byte)
+  bool trailer;    // verify: the init column carries the block's stored
+                   // (masked) crc, read at fetch time; the CRC starts at 0
   uint64_t c_off;  // per lane
   uint32_t c_len, c_init;
   uint32_t cj[S];  // next cache index per group (uniform)
@@ -301,7 +307,14 @@ struct DescSource {
     if ((lane / G) == static_cast<uint32_t>(g) && s < count) {
       c_off = __builtin_nontemporal_load(offsets + s);
       c_len = __builtin_nontemporal_load(lengths + s) + extra;
-      c_init = inits ? __builtin_nontemporal_load(inits + s) : 0u;
+      if (trailer) {
+        // ReadBlock's trailer: LE32 at n + 1 (format.cc:91-93), any alignment
+        const uint8_t* t = base + c_off + (c_len - extra) + 1;
+        c_init = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) |
+                 (uint32_t(t[3]) << 24);
+      } else {
+        c_init = inits ? __builtin_nontemporal_load(inits + s) : 0u;
+      }
     }
   }
   // Descriptor of span s, group g's next span (spans are visited in order,
@@ -328,6 +341,7 @@ struct StridedSource {
   uint32_t length;
   uint32_t init;
   uint64_t count;
+  static constexpr bool trailer = false;
   __device__ __forceinline__ void reset() {}
   __device__ __forceinline__ void desc(int, uint64_t s, uint64_t, uint32_t, uint64_t& start,
                                        uint32_t& len, uint32_t& ini) const {
@@ -421,7 +435,18 @@ __device__ __forceinline__ T gsel(bool hi, T v0, T v1) {
 // an invalid one) loads the 4 KiB at `dummy`, so EVERY slot issues exactly
 // NL vector loads and the ring stays regular.
 __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, const void* dummy,
-                                          u32x4 (&d)[NL]) {
+                                          u32x4 (&d)[NLT]) {
+  // the ragged-tail chunk of each group's segment (the dummy if none): all
+  // lanes of a group read the same 16 bytes
+  uint64_t tail_g[S];
+#pragma unroll
+  for (int g = 0; g < S; ++g) {
+    const uint32_t hn = static_cast<uint32_t>(s[g].start & 15u) + s[g].n();
+    tail_g[g] = ((s[g].flags() & kSlotValid) && (hn & 15u))
+                    ? (s[g].start & ~uint64_t(15)) + (hn & ~15u)
+                    : reinterpret_cast<uint64_t>(dummy);
+  }
+  d[NL] = *reinterpret_cast<g_u32x4*>(gsel(lane >= static_cast<uint32_t>(G), tail_g[0], tail_g[1]));
   uint32_t pad_g[S];
   uint64_t base_g[S];
 #pragma unroll
@@ -507,14 +532,9 @@ __device__ __forceinline__ uint32_t fold_groups(uint32_t (&r)[K], uint32_t lane)
   return v;
 }
 
-// Feeds the ragged tail of a group's segment (uniform): bytes [o, e) of the
-// 16-byte chunk at e0.
-__device__ __forceinline__ uint32_t feed_tail(uint32_t s0, uint32_t reg, uint64_t e0, uint32_t o,
-                                              uint32_t e) {
-  const uint32_t* tp = reinterpret_cast<const uint32_t*>(e0);
-  uint32_t t[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) t[j] = (4u * j < e) ? tp[j] : 0u;
+// Feeds bytes [o, e) of a 16-byte chunk held as words t[0..3].
+__device__ __forceinline__ uint32_t feed_tail_words(uint32_t s0, uint32_t reg, const uint32_t (&t)[4],
+                                                    uint32_t o, uint32_t e) {
   uint32_t i = o;
   if (o == 0) {
 #pragma unroll
@@ -531,20 +551,31 @@ __device__ __forceinline__ uint32_t feed_tail(uint32_t s0, uint32_t reg, uint64_
   return reg;
 }
 
+// The same for the chunk at e0 in memory (only the words that hold bytes
+// below e are read).
+__device__ __forceinline__ uint32_t feed_tail(uint32_t s0, uint32_t reg, uint64_t e0, uint32_t o,
+                                              uint32_t e) {
+  const uint32_t* tp = reinterpret_cast<const uint32_t*>(e0);
+  uint32_t t[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t[j] = (4u * j < e) ? tp[j] : 0u;
+  return feed_tail_words(s0, reg, t, o, e);
+}
+
 // Processes one segment pair whose chunks are in d (already waited for).
 // For each group: `chain` carries the crc from segment to segment of a
 // span; when the segment completes its span, crc[g] is the span's crc and
 // done[g] is set.
-__device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], uint32_t s0,
+__device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NLT], uint32_t s0,
                                             uint32_t lane, uint32_t (&chain)[S],
-                                            uint32_t (&crc)[S], bool (&done)[S]) {
+                                            uint32_t (&crc)[S], bool (&done)[S], bool trailer) {
   const bool hi = lane >= static_cast<uint32_t>(G);
   const uint32_t gl = lane & (G - 1);
   uint32_t init[S], h[S], hn[S];
   bool main_g[S], fast = true, any_main = false;
 #pragma unroll
   for (int g = 0; g < S; ++g) {
-    init[g] = (s[g].flags() & kSlotFirst) ? s[g].init : chain[g];
+    init[g] = (s[g].flags() & kSlotFirst) ? (trailer ? 0u : s[g].init) : chain[g];
     h[g] = static_cast<uint32_t>(s[g].start & 15u);
     hn[g] = h[g] + s[g].n();
     main_g[g] = (s[g].flags() & kSlotValid) && hn[g] >= 16u;
@@ -657,8 +688,12 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NL], 
   for (int g = 0; g < S; ++g) {
     const uint32_t e = hn[g] & 15u;
     if ((s[g].flags() & kSlotValid) && e != 0u) {
-      const uint64_t e0 = (s[g].start & ~uint64_t(15)) + (hn[g] & ~15u);
-      reg[g] = uni(feed_tail(s0, reg[g], e0, hn[g] < 16u ? h[g] : 0u, e));
+      // the tail chunk came with the slot (d[NL], the same in the group's lanes)
+      const uint32_t t[4] = {static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].x, g * G)),
+                             static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].y, g * G)),
+                             static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].z, g * G)),
+                             static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].w, g * G))};
+      reg[g] = uni(feed_tail_words(s0, reg[g], t, hn[g] < 16u ? h[g] : 0u, e));
     }
     const uint32_t c = ~reg[g];
     done[g] = (s[g].flags() & kSlotLast) != 0u;
@@ -700,7 +735,7 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
     for (int g = 0; g < S; ++g) f |= sl[g].meta;
     return (f & (kSlotValid << 16)) != 0u;
   };
-  auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[NL]) {
+  auto finish = [&](const Slot (&sl)[S], u32x4 (&d)[NLT]) {
     uint32_t crc[S];
     bool done[S];
     // an opaque copy of the lane id: the lane predicates derived from it
@@ -710,17 +745,18 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 #if WIPDB_OPAQUE_LANE
     asm volatile("" : "+v"(ln));
 #endif
-    process_seg(sl, d, s0, ln, chain, crc, done);
+    process_seg(sl, d, s0, ln, chain, crc, done, src.trailer);
 #pragma unroll
     for (int g = 0; g < S; ++g)
-      if (done[g]) emit(wave * S + g + static_cast<uint64_t>(sl[g].ord) * stride, crc[g], g);
+      if (done[g])
+        emit(wave * S + g + static_cast<uint64_t>(sl[g].ord) * stride, crc[g], g, sl[g].init);
   };
 
 #if WIPDB_SLOTS == 3
   // Three slots: while one pair is processed the next two pairs' loads are
   // in flight.
   Slot sA[S], sB[S], sC[S];
-  u32x4 bA[NL], bB[NL], bC[NL];
+  u32x4 bA[NLT], bB[NLT], bC[NLT];
   next(sA);
   issue_seg(sA, lane, dummy, bA);
   next(sB);
@@ -744,7 +780,7 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 #else
   // Two slots: while one pair is processed the other's loads are in flight.
   Slot sA[S], sB[S];
-  u32x4 bA[NL], bB[NL];
+  u32x4 bA[NLT], bB[NLT];
   next(sA);
   issue_seg(sA, lane, dummy, bA);
   for (;;) {
@@ -809,10 +845,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  DescSource src{base, offsets, lengths, inits, count, 0u, 0, 0, 0, {0, 0}};
+  DescSource src{base, offsets, lengths, inits, count, 0u, false, 0, 0, 0, {0, 0}};
   const bool msk = (flags & kFlagMask) != 0;
   const bool skip = (flags & kFlagSkipSmall) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, skip, [&](uint64_t span, uint32_t crc, int g) {
+  run_waves(src, wave_id(), grid_waves(), tab, skip,
+            [&](uint64_t span, uint32_t crc, int g, uint32_t) {
     if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
 }
@@ -826,7 +863,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
   load_tables(lds, tab);
   StridedSource src{base, stride_bytes, length, init, count};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, false, [&](uint64_t span, uint32_t crc, int g) {
+  run_waves(src, wave_id(), grid_waves(), tab, false,
+            [&](uint64_t span, uint32_t crc, int g, uint32_t) {
     if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
 }
@@ -839,16 +877,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  DescSource src{base, offsets, lengths, nullptr, count, 1u, 0, 0, 0, {0, 0}};
-  run_waves(src, wave_id(), grid_waves(), tab, false, [&](uint64_t s, uint32_t crc, int g) {
-    if (group_leader(g)) {
-      const uint8_t* t = base + offsets[s] + lengths[s] + 1;
-      const uint32_t stored = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) |
-                              (uint32_t(t[3]) << 24);
-      const uint32_t rot = stored - 0xa282ead8u;
-      status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;
-    }
-  });
+  // the stored trailer crc rides in the descriptor cache (fetched with the
+  // offsets, 32 spans at a time), so emitting a status needs no load
+  DescSource src{base, offsets, lengths, nullptr, count, 1u, true, 0, 0, 0, {0, 0}};
+  run_waves(src, wave_id(), grid_waves(), tab, false,
+            [&](uint64_t s, uint32_t crc, int g, uint32_t stored) {
+              if (group_leader(g)) {
+                const uint32_t rot = stored - 0xa282ead8u;
+                status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;
+              }
+            });
 }
 
 #include "crc32c_small.inc"
