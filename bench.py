@@ -161,10 +161,11 @@ def main():
 
     eng = Engine(local)
     first, nblk = block_shard(rank, world, a.blocks)  # weak scaling, no collective
-    # diagnostic spans longer than the 4 KiB pitch (--len > 4096) run past the
-    # last block: give them slack so every span stays inside the allocation
-    slack = (max(0, a.len - BLOCK) + 4095) // 4096 * 4096
-    data = torch.empty(nblk * BLOCK + slack, dtype=torch.uint8, device=dev)
+    # diagnostic spans longer than the 4 KiB pitch (--len > 4096) or a wider
+    # --stride run past nblk * 4 KiB: size the buffer so every span stays
+    # inside the allocation
+    need = max(nblk * BLOCK, (nblk - 1) * max(a.stride, 0) + a.len)
+    data = torch.empty((need + 4095) // 4096 * 4096, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     if a.fill == "zero":
         data.zero_()

@@ -174,6 +174,35 @@ def test_segment_and_large_spans(engine, oracle):
     np.testing.assert_array_equal(got, oracle.batch(buf, offs, ln, ini))
 
 
+def test_near_4k_lengths_every_pad(engine, oracle):
+    """Every length 2960..4128 (segment pads 0..69 chunks, ragged tails 0..15)
+    at 17 start alignments with inits: the short-pad and full-grid issue
+    paths and the tail chunk loaded with the slot."""
+    rng = np.random.default_rng(31)
+    buf = rng.integers(0, 256, 4 << 20, dtype=np.uint8)
+    lens = np.repeat(np.arange(2960, 4129, dtype=np.uint32), 17)
+    offs = (np.tile(np.arange(17, dtype=np.uint64), 4129 - 2960)
+            + rng.integers(0, 64, lens.size).astype(np.uint64) * 16 * 1024 % (buf.size - 8192))
+    inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    inits[::3] = 0
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
+
+
+@pytest.mark.parametrize("count", [1, 2, 31, 32, 33, 255, 8191, 8192, 8193, 24581, 40000])
+def test_batch_counts_work_sharing(engine, oracle, count):
+    """Batch sizes around the grid's round (8192 groups on 256 CUs) and the
+    workgroup's 32-span round: every span is computed once and lands in its
+    own output slot, whatever batch size the LDS work counter hands out."""
+    rng = np.random.default_rng(count)
+    buf = rng.integers(0, 256, 16 << 20, dtype=np.uint8)
+    lens = rng.integers(0, 9000, count).astype(np.uint32)
+    offs = rng.integers(0, buf.size - 9000, count).astype(np.uint64)
+    inits = rng.integers(0, 2**32, size=count, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
+
+
 def test_zipf_mixed_sst_packing(engine, oracle):
     rng = np.random.default_rng(13)
     buckets = np.array([512, 1024, 2048, 4096, 8192, 16384, 32768, 65536])

@@ -48,7 +48,8 @@ constexpr uint32_t kLdsShiftTables = 6;
 //  [0, 24 KiB)    shift tables: 6 x [4 byte positions][256] u32 -- below
 //                 64 KiB so a compile-time table base fits the 16-bit
 //                 ds_read offset field.
-//  [24 KiB, +1 KiB) inv_top (256 u32), then head0 (16 u32).
+//  [24 KiB, +1 KiB) inv_top (256 u32), then head0 (16 u32), then the
+//                 workgroup's work counter (one u32).
 //  [32 KiB, 160 KiB) slicing-by-4 tables T0..T3, 32 replicas: entry
 //                 (t, b, lane) at 32 KiB + (t >> 1) * 64 KiB + b * 256 +
 //                 (t & 1) * 128 + (lane & 31) * 4.  Lane l only ever reads
@@ -59,6 +60,7 @@ constexpr uint32_t kLdsShiftTables = 6;
 constexpr uint32_t kLdsShift = 0;
 constexpr uint32_t kLdsInvTop = kLdsShift + kLdsShiftTables * 4096;   // 24 KiB
 constexpr uint32_t kLdsHead0 = kLdsInvTop + 1024;
+constexpr uint32_t kLdsWork = kLdsHead0 + 64;  // the workgroup's work counter (u32)
 constexpr uint32_t kLdsMain = 32768;
 constexpr uint32_t kLdsBytes = kLdsMain + 4 * 32768;            // 160 KiB
 

@@ -34,8 +34,11 @@
 //     So any offset/length/init is bit-exact.
 //   * latency hiding: persistent grid (1 workgroup of 16 waves per CU), each
 //     wave walks its segment pairs through a register ring (the next
-//     segments' loads are in flight while one is computed); 32 span
+//     segments' loads are in flight while one is computed); up to 32 span
 //     descriptors per group are fetched per vector load.
+//   * load balance: a workgroup's 32 groups take its spans from an LDS work
+//     counter in guided batches (WorkShare), so the waves the SIMD
+//     arbitration favours take more spans and mixed sizes even out.
 //   * the wave loop keeps segment geometry in 32-bit offsets and counts
 //     spans down: uniform 64-bit compares become VALU compares moved to SCC,
 //     which hipcc 7.2 mis-scheduled in this loop.
@@ -80,11 +83,40 @@
 #ifndef WIPDB_LEAN_ISSUE
 #define WIPDB_LEAN_ISSUE 1
 #endif
+// WIPDB_LEAN_PAD: immediate-offset issue for segments with a short pad too
+#ifndef WIPDB_LEAN_PAD
+#define WIPDB_LEAN_PAD 1
+#endif
+// WIPDB_SHORT_PAD: a CRC path for segments whose span starts in chain 0
+#ifndef WIPDB_SHORT_PAD
+#define WIPDB_SHORT_PAD 1
+#endif
+// WIPDB_PAR_TAIL: both groups' ragged tails fed in the same instructions
+#ifndef WIPDB_PAR_TAIL
+#define WIPDB_PAR_TAIL 1
+#endif
+// WIPDB_DYN: the groups of a workgroup share its spans through an LDS work
+// counter (guided batches) instead of walking fixed stride-apart lists
+#ifndef WIPDB_DYN
+#define WIPDB_DYN 1
+#endif
+// WIPDB_TIMELINE diagnostic: the spans kernel stamps the constant-rate wall
+// clock per workgroup (entry, tables in LDS) and per wave (done) into
+// g_timeline; hcrc_debug_timeline copies it out (scripts/timeline_probe.py)
+#ifndef WIPDB_TIMELINE
+#define WIPDB_TIMELINE 0
+#endif
 
 
 
 namespace wipdb {
 namespace dev {
+
+#if WIPDB_TIMELINE
+constexpr int kTimelineWGs = 1024;
+constexpr int kTimelineStride = 2 + kWaves;  // entry, tables, done per wave
+__device__ uint64_t g_timeline[kTimelineWGs * kTimelineStride];
+#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
@@ -317,6 +349,35 @@ struct DescSource {
       }
     }
   }
+  // Work sharing (WIPDB_DYN): group g grabbed units [ub, ub + nb) of its
+  // workgroup's share; lane g*G + j loads the descriptor of unit ub + j.
+  template <typename WS>
+  __device__ __forceinline__ void fetch_units(int g, uint32_t ub, uint32_t nb, const WS& ws,
+                                              uint32_t lane) {
+    const uint32_t j = lane & (G - 1);
+    if ((lane / G) == static_cast<uint32_t>(g) && j < nb) {
+      const uint64_t sp = ws.span_of(ub + j);
+      c_off = __builtin_nontemporal_load(offsets + sp);
+      c_len = __builtin_nontemporal_load(lengths + sp) + extra;
+      if (trailer) {
+        const uint8_t* t = base + c_off + (c_len - extra) + 1;
+        c_init = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) |
+                 (uint32_t(t[3]) << 24);
+      } else {
+        c_init = inits ? __builtin_nontemporal_load(inits + sp) : 0u;
+      }
+    }
+  }
+  // Entry j of group g's batch (uniform j).
+  __device__ __forceinline__ void at(int g, uint32_t j, uint64_t, uint64_t& start, uint32_t& len,
+                                     uint32_t& init) const {
+    const uint32_t l = g * G + j;
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c_off), l);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(c_off >> 32), l);
+    start = reinterpret_cast<uint64_t>(base) + ((static_cast<uint64_t>(hi) << 32) | lo);
+    len = __builtin_amdgcn_readlane(c_len, l);
+    init = __builtin_amdgcn_readlane(c_init, l);
+  }
   // Descriptor of span s, group g's next span (spans are visited in order,
   // `stride` apart): the cache index advances by one, no division.
   __device__ __forceinline__ void desc(int g, uint64_t s, uint64_t stride, uint32_t lane,
@@ -348,6 +409,43 @@ struct StridedSource {
     start = reinterpret_cast<uint64_t>(base) + s * stride_bytes;
     len = length;
     ini = init;
+  }
+  template <typename WS>
+  __device__ __forceinline__ void fetch_units(int, uint32_t, uint32_t, const WS&, uint32_t) {}
+  __device__ __forceinline__ void at(int, uint32_t, uint64_t s, uint64_t& start, uint32_t& len,
+                                     uint32_t& ini) const {
+    start = reinterpret_cast<uint64_t>(base) + s * stride_bytes;
+    len = length;
+    ini = init;
+  }
+};
+
+// A workgroup's share of the batch: unit u is span (u / 32) * stride + wg0 +
+// u % 32 -- the spans the static schedule gives the workgroup's 32 groups,
+// round by round -- and its groups take units from an LDS counter in
+// guided batches (half the per-group share of what is left, at most a
+// descriptor load's 32, at least 1), so a group that the SIMD's arbitration
+// serves faster simply takes more spans and all finish together.
+struct WorkShare {
+  uint64_t stride;  // spans per round of the grid (groups in the grid)
+  uint64_t wg0;     // this workgroup's first span
+  uint32_t units;   // units of this workgroup
+  __device__ __forceinline__ uint64_t span_of(uint32_t u) const {
+    return static_cast<uint64_t>(u >> 5) * stride + wg0 + (u & 31u);
+  }
+  __device__ __forceinline__ void init(uint64_t count) {
+    stride = grid_groups();
+    wg0 = static_cast<uint64_t>(blockIdx.x) * kSpansPerWG;
+    units = 0u;
+    if (count > wg0) {
+      const uint64_t r = count - wg0;
+      const uint64_t full = r / stride;
+      const uint64_t part = r - full * stride;
+      units = static_cast<uint32_t>(full * kSpansPerWG + (part < kSpansPerWG ? part : kSpansPerWG));
+    }
+  }
+  static __device__ __forceinline__ uint64_t grid_groups() {
+    return static_cast<uint64_t>(gridDim.x) * kSpansPerWG;
   }
 };
 
@@ -409,6 +507,87 @@ struct SegCursor {
       if (left != 0u) src.desc(g, s0 + static_cast<uint64_t>(ord) * stride, stride, lane, start,
                                rest, init);
       skip_small(src, g, s0, stride, lane);
+    } else {
+      start += n;
+      rest -= n;
+      first = 0u;
+    }
+    return sl;
+  }
+};
+
+// The work-sharing cursor (WIPDB_DYN): like SegCursor, but the group's
+// next span is the next unit of its grabbed batch, and an exhausted batch is
+// replaced from the workgroup's LDS counter.  Slot.ord carries the unit.
+template <typename Src>
+struct DynCursor {
+  uint64_t start;
+  uint32_t rest, init, first, left;  // left: 1 while the group has a current span
+  uint32_t u, ub, ue;                // current unit; grabbed batch [ub, ue)
+  bool skip;
+
+  // Makes unit u (the next one) current, grabbing a batch when needed.
+  __device__ __forceinline__ void load(Src& src, int g, const WorkShare& ws, uint32_t lane) {
+    if (u >= ue) {
+      // guided: half of this group's share of what is left (ue is where
+      // the counter stood at the last grab, so this overestimates what is
+      // left and never underestimates the batch)
+      const uint32_t est = ws.units > ue ? ws.units - ue : 0u;
+      uint32_t want = est / (2u * kSpansPerWG);
+      want = want < 1u ? 1u : (want > static_cast<uint32_t>(G) ? static_cast<uint32_t>(G) : want);
+      uint32_t old = 0u;
+      if (lane == static_cast<uint32_t>(g * G))
+        old = __atomic_fetch_add(
+            reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+                static_cast<uintptr_t>(kLdsWork)),
+            want, __ATOMIC_RELAXED);
+      old = uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(old, g * G)));
+      if (old >= ws.units) {
+        left = 0u;
+        ue = ws.units;
+        return;
+      }
+      ub = old;
+      ue = old + want < ws.units ? old + want : ws.units;
+      u = ub;
+      src.fetch_units(g, ub, ue - ub, ws, lane);
+    }
+    left = 1u;
+    src.at(g, u - ub, ws.span_of(u), start, rest, init);
+  }
+  __device__ __forceinline__ void skip_small(Src& src, int g, const WorkShare& ws, uint32_t lane) {
+    while (skip && left != 0u && rest <= kSmallMax) {
+      ++u;
+      load(src, g, ws, lane);
+    }
+  }
+  __device__ __forceinline__ void begin(Src& src, int g, const WorkShare& ws, uint32_t lane,
+                                       bool skip_small_spans) {
+    first = 1u;
+    start = 0;
+    rest = 0;
+    init = 0;
+    u = ub = ue = 0u;
+    left = 0u;
+    skip = skip_small_spans;
+    load(src, g, ws, lane);
+    skip_small(src, g, ws, lane);
+  }
+  __device__ __forceinline__ Slot next(Src& src, int g, const WorkShare& ws, uint32_t lane) {
+    Slot sl{0, 0, 0, 0};
+    if (left == 0u) return sl;
+    const uint32_t room = 4096u - static_cast<uint32_t>(start & 15u);
+    const bool last = rest <= room + 15u;
+    const uint32_t n = last ? rest : room;
+    sl.start = start;
+    sl.init = init;
+    sl.meta = n | ((kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u)) << 16);
+    sl.ord = u;
+    if (last) {
+      first = 1u;
+      ++u;
+      load(src, g, ws, lane);
+      skip_small(src, g, ws, lane);
     } else {
       start += n;
       rest -= n;
@@ -482,6 +661,24 @@ __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, con
     }
     return;
   }
+  if (WIPDB_LEAN_PAD && !X && pad_g[0] < static_cast<uint32_t>(C * G) &&
+      pad_g[1] < static_cast<uint32_t>(C * G)) {
+    // a short pad (spans of 3 KiB+ -- a 4 KiB block minus its trailer):
+    // only chain 0's loads can fall in front of the span, so chains 1.. load
+    // at immediate offsets from one shifted lane address
+    const int32_t sh = static_cast<int32_t>(C * gl) - static_cast<int32_t>(pad);
+    g_u32x4* bl = b + sh;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      if (i < C) {
+        const int32_t q = sh + i;
+        d[i] = b[q > 0 ? q : 0];
+      } else {
+        d[i] = bl[C * G * (i / C) + i % C];
+      }
+    }
+    return;
+  }
 #endif
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
@@ -532,20 +729,18 @@ __device__ __forceinline__ uint32_t fold_groups(uint32_t (&r)[K], uint32_t lane)
   return v;
 }
 
-// Feeds bytes [o, e) of a 16-byte chunk held as words t[0..3].
-__device__ __forceinline__ uint32_t feed_tail_words(uint32_t s0, uint32_t reg, const uint32_t (&t)[4],
+// Feeds bytes [o, e) of a 16-byte chunk held as words t0..t3.
+__device__ __forceinline__ uint32_t feed_tail_words(uint32_t s0, uint32_t reg, uint32_t t0,
+                                                    uint32_t t1, uint32_t t2, uint32_t t3,
                                                     uint32_t o, uint32_t e) {
   uint32_t i = o;
   if (o == 0) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      if (4u * j + 4u <= e) {
-        reg = feed_word(s0, reg, t[j]);
-        i += 4;
-      }
+    if (e >= 4u) reg = feed_word(s0, reg, t0), i = 4u;
+    if (e >= 8u) reg = feed_word(s0, reg, t1), i = 8u;
+    if (e >= 12u) reg = feed_word(s0, reg, t2), i = 12u;
   }
   for (; i < e; ++i) {
-    const uint32_t wd = i < 4 ? t[0] : (i < 8 ? t[1] : (i < 12 ? t[2] : t[3]));
+    const uint32_t wd = i < 4 ? t0 : (i < 8 ? t1 : (i < 12 ? t2 : t3));
     reg = feed_byte(s0, reg, (wd >> (8 * (i & 3))) & 0xffu);
   }
   return reg;
@@ -556,10 +751,11 @@ __device__ __forceinline__ uint32_t feed_tail_words(uint32_t s0, uint32_t reg, c
 __device__ __forceinline__ uint32_t feed_tail(uint32_t s0, uint32_t reg, uint64_t e0, uint32_t o,
                                               uint32_t e) {
   const uint32_t* tp = reinterpret_cast<const uint32_t*>(e0);
-  uint32_t t[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) t[j] = (4u * j < e) ? tp[j] : 0u;
-  return feed_tail_words(s0, reg, t, o, e);
+  const uint32_t t0 = tp[0];
+  const uint32_t t1 = e > 4u ? tp[1] : 0u;
+  const uint32_t t2 = e > 8u ? tp[2] : 0u;
+  const uint32_t t3 = e > 12u ? tp[3] : 0u;
+  return feed_tail_words(s0, reg, t0, t1, t2, t3, o, e);
 }
 
 // Processes one segment pair whose chunks are in d (already waited for).
@@ -572,7 +768,7 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NLT],
   const bool hi = lane >= static_cast<uint32_t>(G);
   const uint32_t gl = lane & (G - 1);
   uint32_t init[S], h[S], hn[S];
-  bool main_g[S], fast = true, any_main = false;
+  bool main_g[S], fast = true, any_main = false, short_pad = !X, any_h = false;
 #pragma unroll
   for (int g = 0; g < S; ++g) {
     init[g] = (s[g].flags() & kSlotFirst) ? (trailer ? 0u : s[g].init) : chain[g];
@@ -580,6 +776,9 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NLT],
     hn[g] = h[g] + s[g].n();
     main_g[g] = (s[g].flags() & kSlotValid) && hn[g] >= 16u;
     fast = fast && main_g[g] && h[g] == 0u && hn[g] == 4096u;
+    // the span's first chunk falls in chain 0 (pad < C*G chunks)
+    short_pad = short_pad && main_g[g] && (hn[g] >> 4) > kSegChunks - C * G;
+    any_h = any_h || h[g] != 0u;
     any_main = any_main || main_g[g];
   }
   uint32_t reg[S];
@@ -612,6 +811,54 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NLT],
       if constexpr (C > 1) feed_chunks<1>(s0, r, d);
       if constexpr (C > 2) feed_chunks<2>(s0, r, d);
       if constexpr (C > 3) feed_chunks<3>(s0, r, d);
+    } else if (WIPDB_SHORT_PAD && short_pad) {
+      // both groups' spans start in chain 0 (segments of 3 KiB+, e.g. a 4 KiB
+      // block minus its trailer): the general path below with k0 = 0 known,
+      // so only loads 0..C-1 of lane l0 can need the head mask, only chain 0
+      // takes the injection, and only chain 0 of the lanes in front of l0 is
+      // all virtual
+      uint32_t pad_g[S], inj_g[S], m_g[S][4];
+#pragma unroll
+      for (int g = 0; g < S; ++g) {
+        pad_g[g] = kSegChunks - (hn[g] >> 4);
+        const uint32_t hh = h[g];
+        inj_g[g] = (init[g] == 0u) ? lds_ld(kLdsHead0 + (hh << 2)) : unshift_bytes(s0, ~init[g], hh);
+        m_g[g][0] = hh == 0 ? ~0u : (hh >= 4 ? 0u : (~0u << (8 * hh)));
+        m_g[g][1] = hh <= 4 ? ~0u : (hh >= 8 ? 0u : (~0u << (8 * (hh - 4))));
+        m_g[g][2] = hh <= 8 ? ~0u : (hh >= 12 ? 0u : (~0u << (8 * (hh - 8))));
+        m_g[g][3] = hh <= 12 ? ~0u : (~0u << (8 * (hh - 12)));
+      }
+      const uint32_t pad = gsel(hi, pad_g[0], pad_g[1]);
+      const uint32_t inj = gsel(hi, inj_g[0], inj_g[1]);
+      const uint32_t l0 = pad / C, j0 = pad % C;
+      const bool at0 = gl == l0;
+      if (any_h) {
+        const uint32_t m0 = gsel(hi, m_g[0][0], m_g[1][0]), m1 = gsel(hi, m_g[0][1], m_g[1][1]);
+        const uint32_t m2 = gsel(hi, m_g[0][2], m_g[1][2]), m3 = gsel(hi, m_g[0][3], m_g[1][3]);
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          const bool mj = at0 && j0 == static_cast<uint32_t>(j);
+          d[j].x &= mj ? m0 : ~0u;
+          d[j].y &= mj ? m1 : ~0u;
+          d[j].z &= mj ? m2 : ~0u;
+          d[j].w &= mj ? m3 : ~0u;
+        }
+      }
+      if (at0 && j0 == 0u) r[0] = inj;
+      feed_chunks<0>(s0, r, d);
+      if constexpr (C > 1) {
+        if (at0 && j0 == 1u) r[0] = inj;
+        feed_chunks<1>(s0, r, d);
+      }
+      if constexpr (C > 2) {
+        if (at0 && j0 == 2u) r[0] = inj;
+        feed_chunks<2>(s0, r, d);
+      }
+      if constexpr (C > 3) {
+        if (at0 && j0 == 3u) r[0] = inj;
+        feed_chunks<3>(s0, r, d);
+      }
+      if (gl < l0) r[0] = 0u;
     } else {
       // general path: chunk 0 of a group sits at its virtual chunk `pad`
       // (chain k0 = pad / (G*C), lane l0, sub-chunk j0): mask its first h
@@ -683,18 +930,41 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NLT],
     for (int g = 0; g < S; ++g)
       if (main_g[g]) reg[g] = __builtin_amdgcn_readlane(v, g * G);
   }
-  // ragged tails: bytes [o, e) of the chunk at a0 + (hn & ~15)
+  // ragged tails: bytes [o, e) of the chunk at a0 + (hn & ~15).  The tail
+  // chunk came with the slot (d[NL], the same in a group's lanes), so the
+  // lanes of each group feed their group's tail: both tails in the same
+  // instructions
+  uint32_t e_g[S], o_g[S];
+  bool any_tail = false;
 #pragma unroll
   for (int g = 0; g < S; ++g) {
-    const uint32_t e = hn[g] & 15u;
-    if ((s[g].flags() & kSlotValid) && e != 0u) {
-      // the tail chunk came with the slot (d[NL], the same in the group's lanes)
-      const uint32_t t[4] = {static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].x, g * G)),
-                             static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].y, g * G)),
-                             static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].z, g * G)),
-                             static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].w, g * G))};
-      reg[g] = uni(feed_tail_words(s0, reg[g], t, hn[g] < 16u ? h[g] : 0u, e));
+    e_g[g] = (s[g].flags() & kSlotValid) ? (hn[g] & 15u) : 0u;
+    o_g[g] = hn[g] < 16u ? h[g] : 0u;
+    any_tail = any_tail || e_g[g] != 0u;
+  }
+#if WIPDB_PAR_TAIL
+  if (any_tail) {
+    const uint32_t rt = feed_tail_words(s0, gsel(hi, reg[0], reg[1]), d[NL].x, d[NL].y, d[NL].z,
+                                        d[NL].w, gsel(hi, o_g[0], o_g[1]), gsel(hi, e_g[0], e_g[1]));
+#pragma unroll
+    for (int g = 0; g < S; ++g)
+      if (e_g[g] != 0u) reg[g] = uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(rt, g * G)));
+  }
+#else
+#pragma unroll
+  for (int g = 0; g < S; ++g) {
+    if (e_g[g] != 0u) {
+      const uint32_t t0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].x, g * G));
+      const uint32_t t1 = static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].y, g * G));
+      const uint32_t t2 = static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].z, g * G));
+      const uint32_t t3 = static_cast<uint32_t>(__builtin_amdgcn_readlane(d[NL].w, g * G));
+      reg[g] = uni(feed_tail_words(s0, reg[g], t0, t1, t2, t3, o_g[g], e_g[g]));
     }
+  }
+  (void)any_tail;
+#endif
+#pragma unroll
+  for (int g = 0; g < S; ++g) {
     const uint32_t c = ~reg[g];
     done[g] = (s[g].flags() & kSlotLast) != 0u;
     crc[g] = c;
@@ -711,15 +981,29 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l4 = (threadIdx.x & 31u) * 4u;
   const uint32_t s0 = l4 | ((l4 | 0x80u) << 8) | (1u << 24);
-  const uint64_t stride = waves * S;
+  [[maybe_unused]] const uint64_t stride = waves * S;
 
   src.reset();
+#if WIPDB_DYN
+  WorkShare ws;
+  ws.init(src.count);
+  DynCursor<Src> cur[S];
+  auto span_of = [&](int, uint32_t ord) { return ws.span_of(ord); };
+#else
   SegCursor<Src> cur[S];
+  auto span_of = [&](int g, uint32_t ord) {
+    return wave * S + g + static_cast<uint64_t>(ord) * stride;
+  };
+#endif
   uint32_t chain[S];
   uint32_t live = 0;  // groups with spans left (checked once: all zero -> return)
 #pragma unroll
   for (int g = 0; g < S; ++g) {
+#if WIPDB_DYN
+    cur[g].begin(src, g, ws, lane, skip_small);
+#else
     cur[g].begin(src, g, wave * S + g, stride, lane, skip_small);
+#endif
     chain[g] = 0;
     live |= cur[g].left;
   }
@@ -727,7 +1011,12 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 
   auto next = [&](Slot (&sl)[S]) {
 #pragma unroll
-    for (int g = 0; g < S; ++g) sl[g] = cur[g].next(src, g, wave * S + g, stride, lane);
+    for (int g = 0; g < S; ++g)
+#if WIPDB_DYN
+      sl[g] = cur[g].next(src, g, ws, lane);
+#else
+      sl[g] = cur[g].next(src, g, wave * S + g, stride, lane);
+#endif
   };
   auto valid = [](const Slot (&sl)[S]) {
     uint32_t f = 0;
@@ -749,7 +1038,7 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 #pragma unroll
     for (int g = 0; g < S; ++g)
       if (done[g])
-        emit(wave * S + g + static_cast<uint64_t>(sl[g].ord) * stride, crc[g], g, sl[g].init);
+        emit(span_of(g, sl[g].ord), crc[g], g, sl[g].init);
   };
 
 #if WIPDB_SLOTS == 3
@@ -818,6 +1107,7 @@ __device__ __forceinline__ void load_tables(uint8_t* lds, const DevTables* __res
   for (uint32_t i = tid; i < 256u; i += nthr) inv[i] = tab->inv_top[i];
   uint32_t* hd = reinterpret_cast<uint32_t*>(lds + kLdsHead0);
   for (uint32_t i = tid; i < 16u; i += nthr) hd[i] = tab->head0[i];
+  if (tid == 0u) *reinterpret_cast<uint32_t*>(lds + kLdsWork) = 0u;
   __syncthreads();
 }
 
@@ -844,7 +1134,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags,
     const DevTables* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+#if WIPDB_TIMELINE
+  const uint64_t t_entry = wall_clock64();
+#endif
   load_tables(lds, tab);
+#if WIPDB_TIMELINE
+  uint64_t* tl = g_timeline + static_cast<uint64_t>(blockIdx.x) * kTimelineStride;
+  const bool stamp = blockIdx.x < static_cast<uint32_t>(kTimelineWGs) && (threadIdx.x & 63u) == 0u;
+  if (stamp && threadIdx.x == 0u) {
+    tl[0] = t_entry;
+    tl[1] = wall_clock64();
+  }
+#endif
   DescSource src{base, offsets, lengths, inits, count, 0u, false, 0, 0, 0, {0, 0}};
   const bool msk = (flags & kFlagMask) != 0;
   const bool skip = (flags & kFlagSkipSmall) != 0;
@@ -852,6 +1153,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
             [&](uint64_t span, uint32_t crc, int g, uint32_t) {
     if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
+#if WIPDB_TIMELINE
+  if (stamp) tl[2 + (threadIdx.x >> 6)] = wall_clock64();
+#endif
 }
 
 // Fixed-size blocks at a fixed stride.
@@ -930,3 +1234,14 @@ __global__ __launch_bounds__(256) void fill_splitmix64_kernel(uint64_t* __restri
 
 }  // namespace dev
 }  // namespace wipdb
+
+#if WIPDB_TIMELINE
+// Diagnostic (variant builds only): copy the last spans launch's stamps.
+extern "C" int hcrc_debug_timeline(uint64_t* dst, size_t n) {
+  const size_t cap = static_cast<size_t>(wipdb::dev::kTimelineWGs) * wipdb::dev::kTimelineStride;
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(wipdb::dev::g_timeline), n * 8) == hipSuccess
+             ? static_cast<int>(n) : -1;
+}
+#endif
