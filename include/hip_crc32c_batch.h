@@ -71,10 +71,14 @@ extern "C" {
 #define HCRC_DEVICE_PTRS 0x1  /* all array/data pointers are device memory  */
 #define HCRC_MASK_OUTPUT 0x2  /* write Mask(crc) instead of crc             */
 /* Spans of at most 1024 bytes are checksummed by the small-span kernel
- * (8 per wave slot) instead of a whole 4 KiB group segment each: a partition
- * pass compacts them, stream-ordered scratch (hipMallocAsync).  Same
- * results; pays off for batches with many short spans (WAL records, small
- * meta blocks).  hcrc_batch on host memory chooses it by itself. */
+ * (8 per wave slot) instead of a whole 4 KiB group segment each, and so are
+ * the last 16..1024 bytes of a span that just overruns one 4 KiB segment (a
+ * table block: 4096 bytes + its last entry + the type byte): the spans
+ * kernel stops after the first segment and the small kernel continues from
+ * its partial CRC.  A partition pass compacts them, stream-ordered scratch
+ * (hipMallocAsync).  Same results; pays off for batches with many short
+ * spans (WAL records, small meta blocks) or table blocks.  hcrc_batch on
+ * host memory chooses it by itself.  count < 2^31 per call. */
 #define HCRC_SPLIT_SMALL 0x4
 
 typedef struct hcrc_ctx hcrc_ctx;

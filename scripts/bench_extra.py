@@ -122,6 +122,35 @@ def run_mixed(eng, d, stream, rng, gib):
     return res
 
 
+def run_tblocks(eng, d, stream, rng, gib=4.0):
+    """Table-block-shaped device batch: data blocks as TableBuilder cuts them
+    (4096 + the last entry: 4097..4225 bytes with the type byte), packed like
+    an SST (contents + type, then the 4-byte crc), device-resident; spans
+    kernel alone and with HCRC_SPLIT_SMALL (remainders to the small kernel)."""
+    nbytes = int(gib * 2**30)
+    dbuf = torch.empty(nbytes + 8192, dtype=torch.uint8, device=d)
+    eng.fill_splitmix64_device(dbuf, 11, stream=stream.cuda_stream)
+    n = nbytes // 4165
+    lens = rng.integers(4097, 4226, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 4)[:-1]]).astype(np.uint64)
+    do, dl = dev(offs, d), dev(lens, d)
+    res = {"config": "table blocks 4097..4225 B (contents + type), SST-packed, device-resident",
+           "spans": int(n), "bytes": int(lens.sum())}
+    ref = None
+    for split in (False, True):
+        out = torch.empty(n, dtype=torch.int32, device=d)
+        t = time_kernel(lambda: eng.batch_device(dbuf, do, dl, None, out, stream=stream.cuda_stream,
+                                                     split_small=split), stream, 10)
+        got = out.cpu().numpy()
+        if ref is None:
+            ref = got
+        res["split" if split else "spans_kernel"] = {
+            "GiBps": round(float(lens.sum()) / t / 2**30, 1), "ms": round(t * 1e3, 4),
+            "same_as_unsplit": bool((got == ref).all())}
+    del dbuf
+    return res
+
+
 def run_verify(eng, d, stream, rng, nblk=1 << 20):
     """Read side, device-resident (hcrc_verify_async, ReadBlock's check):
     1 M blocks of 4096 bytes on disk = 4091 contents + type byte + masked
@@ -218,6 +247,8 @@ def main():
                 r = run_mixed(eng, d, stream, rng, a.mixed_gib)
             elif w == "verify":
                 r = run_verify(eng, d, stream, rng)
+            elif w == "tblocks":
+                r = run_tblocks(eng, d, stream, rng)
             elif w == "sst":
                 r = run_sst(eng, rng, a.ssts)
             elif w == "host4k":

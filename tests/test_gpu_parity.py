@@ -158,6 +158,44 @@ def test_split_small_boundaries_and_mix(engine, oracle):
     np.testing.assert_array_equal(engine.batch(buf, offs, lens, inits), want)
 
 
+def test_split_remainders(engine, oracle):
+    """HCRC_SPLIT_SMALL cuts a span whose rest after its first segment is
+    16..1024 bytes: the spans kernel leaves the partial CRC, the small
+    kernel finishes it.  Every start alignment, the cut's edges on both
+    sides, inits, masked output, mixed with small and long spans; and a
+    table-block-shaped host batch (4097..4225 B, SST-packed)."""
+    rng = np.random.default_rng(41)
+    buf = rng.integers(0, 256, 16 << 20, dtype=np.uint8)
+    lens, offs = [], []
+    for h in range(16):
+        room = 4096 - h
+        for n in sorted({room + 14, room + 15, room + 16, room + 17, room + 100, room + 1023,
+                         room + 1024, room + 1025, room + 1040, 4097, 4225, 5120, 8192 + 7,
+                         1024, 1025, 300, 70001}):
+            lens.append(n)
+            offs.append(int(rng.integers(0, (buf.size - 80000) // 16)) * 16 + h)
+    lens = np.array(lens, np.uint32)
+    offs = np.array(offs, np.uint64)
+    inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    inits[::4] = 0
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits, split=True), want)
+    np.testing.assert_array_equal(
+        _run_device(engine, buf, offs, lens, inits, mask=True, split=True),
+        np.array([oracle.lib.oracle_mask(int(x)) for x in want], np.uint32))
+    # SST-packed table blocks (contents + type byte), host path (auto split)
+    blens, boffs, cur = [], [], 0
+    while cur + 4300 < buf.size // 4:
+        n = int(rng.integers(4097, 4226))
+        boffs.append(cur)
+        blens.append(n)
+        cur += n + 4
+    blens, boffs = np.array(blens, np.uint32), np.array(boffs, np.uint64)
+    want = oracle.batch(buf, boffs, blens)
+    np.testing.assert_array_equal(engine.batch(buf, boffs, blens), want)
+    np.testing.assert_array_equal(_run_device(engine, buf, boffs, blens, split=True), want)
+
+
 def test_segment_and_large_spans(engine, oracle):
     rng = np.random.default_rng(9)
     buf = rng.integers(0, 256, 3 << 20, dtype=np.uint8)

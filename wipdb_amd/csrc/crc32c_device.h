@@ -17,6 +17,22 @@ constexpr uint32_t kFlagMask = 0x2;      // == HCRC_MASK_OUTPUT
 // kernel (HCRC_SPLIT_SMALL, crc32c_small.inc)
 constexpr uint32_t kFlagSkipSmall = 0x4;
 constexpr uint32_t kSmallMax = 1024;
+// spans kernel: a span whose rest after its first 4 KiB segment is at most
+// kSmallMax bytes stops there (its unmasked partial CRC goes to out[i]) and
+// the small-span kernel finishes it (SplitRemainder below)
+constexpr uint32_t kFlagSplitRem = 0x8;
+// small-span list entries that continue a span from out[id] (remainders)
+constexpr uint32_t kSmallIdRem = 0x80000000u;
+
+// The remainder rule, shared by the spans kernel's cursor and the partition
+// kernel: a span of n bytes starting at address a is cut after its first
+// segment (4096 - a % 16 bytes) when what follows is 16..kSmallMax bytes.
+__host__ __device__ constexpr uint32_t SplitRemainder(uint64_t a, uint32_t n) {
+  return (n > kSmallMax && n > 4096u - static_cast<uint32_t>(a & 15u) + 15u &&
+          n - (4096u - static_cast<uint32_t>(a & 15u)) <= kSmallMax)
+             ? 4096u - static_cast<uint32_t>(a & 15u)
+             : 0u;
+}
 
 // Compacted descriptors of a batch's small spans (written by
 // crc32c_partition_kernel, read by crc32c_small_kernel); count is a

@@ -296,7 +296,7 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) {
 // tail hn & 15 bytes after it.  All fields are uniform.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegChunks = 256;
-constexpr uint32_t kSlotFirst = 1u, kSlotLast = 2u, kSlotValid = 4u;
+constexpr uint32_t kSlotFirst = 1u, kSlotLast = 2u, kSlotValid = 4u, kSlotPartial = 8u;
 
 // Kept small: the ring holds several slots per group in SGPRs.
 struct Slot {
@@ -456,6 +456,7 @@ struct SegCursor {
   uint64_t start;
   uint32_t rest, init, first, left;  // left: spans not yet finished, incl. this one
   uint32_t ord;                      // ordinal of the current span
+  uint32_t split;                    // kFlagSkipSmall | kFlagSplitRem
   bool skip;                         // kFlagSkipSmall: small spans are the small kernel's
 
   // With `skip`, step over spans of at most kSmallMax bytes (their ordinals
@@ -471,7 +472,7 @@ struct SegCursor {
   }
 
   __device__ __forceinline__ void begin(Src& src, int g, uint64_t s, uint64_t stride,
-                                       uint32_t lane, bool skip_small_spans) {
+                                       uint32_t lane, uint32_t split_flags) {
     // s < stride always, so this is ceil((count - s) / stride) or 0 -- no compare
     left = static_cast<uint32_t>((src.count + stride - 1 - s) / stride);
     first = 1u;
@@ -479,7 +480,8 @@ struct SegCursor {
     start = 0;
     rest = 0;
     init = 0;
-    skip = skip_small_spans;
+    split = split_flags;
+    skip = (split_flags & kFlagSkipSmall) != 0u;
     if (left != 0u) src.desc(g, s, stride, lane, start, rest, init);
     skip_small(src, g, s, stride, lane);
   }
@@ -494,11 +496,13 @@ struct SegCursor {
     // fold), it is the last segment -- so an unaligned 4 KiB block is one
     // segment, not 4096 - h bytes and an h-byte second one
     const uint32_t room = 4096u - static_cast<uint32_t>(start & 15u);
-    const bool last = rest <= room + 15u;
-    const uint32_t n = last ? rest : room;
+    const bool cut = first && (split & kFlagSplitRem) && SplitRemainder(start, rest) != 0u;
+    const bool last = rest <= room + 15u || cut;
+    const uint32_t n = rest <= room + 15u ? rest : room;
     sl.start = start;
     sl.init = init;
-    sl.meta = n | ((kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u)) << 16);
+    sl.meta = n | ((kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u) |
+                    (cut ? kSlotPartial : 0u)) << 16);
     sl.ord = ord;
     if (last) {
       ++ord;
@@ -524,6 +528,7 @@ struct DynCursor {
   uint64_t start;
   uint32_t rest, init, first, left;  // left: 1 while the group has a current span
   uint32_t u, ub, ue;                // current unit; grabbed batch [ub, ue)
+  uint32_t split;                    // kFlagSkipSmall | kFlagSplitRem
   bool skip;
 
   // Makes unit u (the next one) current, grabbing a batch when needed.
@@ -562,14 +567,15 @@ struct DynCursor {
     }
   }
   __device__ __forceinline__ void begin(Src& src, int g, const WorkShare& ws, uint32_t lane,
-                                       bool skip_small_spans) {
+                                       uint32_t split_flags) {
     first = 1u;
     start = 0;
     rest = 0;
     init = 0;
     u = ub = ue = 0u;
     left = 0u;
-    skip = skip_small_spans;
+    split = split_flags;
+    skip = (split_flags & kFlagSkipSmall) != 0u;
     load(src, g, ws, lane);
     skip_small(src, g, ws, lane);
   }
@@ -577,11 +583,15 @@ struct DynCursor {
     Slot sl{0, 0, 0, 0};
     if (left == 0u) return sl;
     const uint32_t room = 4096u - static_cast<uint32_t>(start & 15u);
-    const bool last = rest <= room + 15u;
-    const uint32_t n = last ? rest : room;
+    // HCRC_SPLIT_SMALL: a span whose rest after this first segment fits the
+    // small kernel stops here (partial CRC, unmasked)
+    const bool cut = first && (split & kFlagSplitRem) && SplitRemainder(start, rest) != 0u;
+    const bool last = rest <= room + 15u || cut;
+    const uint32_t n = rest <= room + 15u ? rest : room;
     sl.start = start;
     sl.init = init;
-    sl.meta = n | ((kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u)) << 16);
+    sl.meta = n | ((kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u) |
+                    (cut ? kSlotPartial : 0u)) << 16);
     sl.ord = u;
     if (last) {
       first = 1u;
@@ -977,7 +987,7 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NLT],
 // and crc uniform).
 template <typename Src, typename Emit>
 __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t waves,
-                                          const void* dummy, bool skip_small, Emit emit) {
+                                          const void* dummy, uint32_t split, Emit emit) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l4 = (threadIdx.x & 31u) * 4u;
   const uint32_t s0 = l4 | ((l4 | 0x80u) << 8) | (1u << 24);
@@ -1000,9 +1010,9 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 #pragma unroll
   for (int g = 0; g < S; ++g) {
 #if WIPDB_DYN
-    cur[g].begin(src, g, ws, lane, skip_small);
+    cur[g].begin(src, g, ws, lane, split);
 #else
-    cur[g].begin(src, g, wave * S + g, stride, lane, skip_small);
+    cur[g].begin(src, g, wave * S + g, stride, lane, split);
 #endif
     chain[g] = 0;
     live |= cur[g].left;
@@ -1038,7 +1048,8 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 #pragma unroll
     for (int g = 0; g < S; ++g)
       if (done[g])
-        emit(span_of(g, sl[g].ord), crc[g], g, sl[g].init);
+        emit(span_of(g, sl[g].ord), crc[g], g, sl[g].init,
+             (sl[g].flags() & kSlotPartial) != 0u);
   };
 
 #if WIPDB_SLOTS == 3
@@ -1148,10 +1159,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
 #endif
   DescSource src{base, offsets, lengths, inits, count, 0u, false, 0, 0, 0, {0, 0}};
   const bool msk = (flags & kFlagMask) != 0;
-  const bool skip = (flags & kFlagSkipSmall) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, skip,
-            [&](uint64_t span, uint32_t crc, int g, uint32_t) {
-    if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
+  run_waves(src, wave_id(), grid_waves(), tab, flags & (kFlagSkipSmall | kFlagSplitRem),
+            [&](uint64_t span, uint32_t crc, int g, uint32_t, bool partial) {
+    // a partial CRC (remainder left to the small kernel) stays unmasked
+    if (group_leader(g)) out[span] = msk && !partial ? mask_crc(crc) : crc;
   });
 #if WIPDB_TIMELINE
   if (stamp) tl[2 + (threadIdx.x >> 6)] = wall_clock64();
@@ -1167,8 +1178,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
   load_tables(lds, tab);
   StridedSource src{base, stride_bytes, length, init, count};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, false,
-            [&](uint64_t span, uint32_t crc, int g, uint32_t) {
+  run_waves(src, wave_id(), grid_waves(), tab, 0u,
+            [&](uint64_t span, uint32_t crc, int g, uint32_t, bool) {
     if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
 }
@@ -1184,8 +1195,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
   // the stored trailer crc rides in the descriptor cache (fetched with the
   // offsets, 32 spans at a time), so emitting a status needs no load
   DescSource src{base, offsets, lengths, nullptr, count, 1u, true, 0, 0, 0, {0, 0}};
-  run_waves(src, wave_id(), grid_waves(), tab, false,
-            [&](uint64_t s, uint32_t crc, int g, uint32_t stored) {
+  run_waves(src, wave_id(), grid_waves(), tab, 0u,
+            [&](uint64_t s, uint32_t crc, int g, uint32_t stored, bool) {
               if (group_leader(g)) {
                 const uint32_t rot = stored - 0xa282ead8u;
                 status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;

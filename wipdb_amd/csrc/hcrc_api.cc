@@ -42,8 +42,8 @@ __global__ void crc32c_verify_kernel(const uint8_t*, const uint64_t*,
 __global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*,
                                   uint64_t);
 __global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
-__global__ void crc32c_partition_kernel(const uint64_t*, const uint32_t*, const uint32_t*,
-                                        uint64_t, SmallList);
+__global__ void crc32c_partition_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
+                                        const uint32_t*, uint64_t, SmallList);
 __global__ void crc32c_small_kernel(const uint8_t*, SmallList, uint32_t*, uint32_t,
                                     const DevTables*);
 }  // namespace dev
@@ -152,16 +152,22 @@ int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
   if (hipMemsetAsync(sl.count, 0, 4, st) != hipSuccess) rc = HCRC_ERR_HIP;
   if (rc == HCRC_OK) {
     const int pgrid = static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8));
-    hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st, off,
-                       len, init, static_cast<uint64_t>(n), sl);
+    hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st,
+                       static_cast<const uint8_t*>(base), off, len, init,
+                       static_cast<uint64_t>(n), sl);
+    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+  }
+  // the spans kernel first: it leaves the partial CRCs of the spans it cuts
+  // (kFlagSplitRem) in out, which the small kernel then continues
+  if (rc == HCRC_OK)
+    rc = LaunchSpansKernel(ctx, base, off, len, init, out, count,
+                           mask | wipdb::dev::kFlagSkipSmall | wipdb::dev::kFlagSplitRem, st);
+  if (rc == HCRC_OK) {
     hipLaunchKernelGGL(wipdb::dev::crc32c_small_kernel, dim3(ctx->num_cu),
                        dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
                        static_cast<const uint8_t*>(base), sl, out, mask, ctx->d_tab);
     rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
   }
-  if (rc == HCRC_OK)
-    rc = LaunchSpansKernel(ctx, base, off, len, init, out, count,
-                           mask | wipdb::dev::kFlagSkipSmall, st);
   if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
   return rc;
 }
@@ -173,18 +179,22 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off,
                 size_t count, int flags, hipStream_t st) {
   if (count == 0) return HCRC_OK;
   const uint32_t mask = static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT);
-  if ((flags & HCRC_SPLIT_SMALL) && count < (size_t(1) << 32))
+  if ((flags & HCRC_SPLIT_SMALL) && count < (size_t(1) << 31))
     return LaunchSplit(ctx, base, off, len, init, out, count, mask, st);
   return LaunchSpansKernel(ctx, base, off, len, init, out, count, mask, st);
 }
 
-// Host pieces: split when enough spans are small for the small kernel to
-// pay for its two extra launches.
+// Host pieces: split when enough spans are small, or just over a segment
+// (a table block of 4 KiB + its last entry: the remainder goes to the small
+// kernel), for the small kernel to pay for its two extra launches.
 constexpr size_t kAutoSplitMin = 256;
 
 int AutoSplit(const uint32_t* lengths, size_t n) {
   size_t small = 0;
-  for (size_t i = 0; i < n && small < kAutoSplitMin; ++i) small += lengths[i] <= wipdb::dev::kSmallMax;
+  for (size_t i = 0; i < n && small < kAutoSplitMin; ++i) {
+    const uint32_t l = lengths[i];
+    small += l <= wipdb::dev::kSmallMax || (l > 4096u + 15u && l <= 4096u + wipdb::dev::kSmallMax);
+  }
   return small >= kAutoSplitMin ? HCRC_SPLIT_SMALL : 0;
 }
 
