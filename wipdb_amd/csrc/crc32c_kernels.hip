@@ -100,6 +100,14 @@
 #ifndef WIPDB_DYN
 #define WIPDB_DYN 1
 #endif
+// WIPDB_GUIDE: guided batch = what is left / (WIPDB_GUIDE * groups sharing);
+// WIPDB_FRESH_EST: read the counter for that instead of the group's last grab
+#ifndef WIPDB_GUIDE
+#define WIPDB_GUIDE 2u
+#endif
+#ifndef WIPDB_FRESH_EST
+#define WIPDB_FRESH_EST 1
+#endif
 // WIPDB_TIMELINE diagnostic: the spans kernel stamps the constant-rate wall
 // clock per workgroup (entry, tables in LDS) and per wave (done) into
 // g_timeline; hcrc_debug_timeline copies it out (scripts/timeline_probe.py)
@@ -534,11 +542,18 @@ struct DynCursor {
   // Makes unit u (the next one) current, grabbing a batch when needed.
   __device__ __forceinline__ void load(Src& src, int g, const WorkShare& ws, uint32_t lane) {
     if (u >= ue) {
-      // guided: half of this group's share of what is left (ue is where
-      // the counter stood at the last grab, so this overestimates what is
-      // left and never underestimates the batch)
-      const uint32_t est = ws.units > ue ? ws.units - ue : 0u;
-      uint32_t want = est / (2u * kSpansPerWG);
+      // guided: a fraction of this group's share of what is left, read
+      // from the counter just before the grab (other groups may take some
+      // in between: the batch only comes out larger than the rule by what
+      // they took)
+#if WIPDB_FRESH_EST
+      const uint32_t at = uni(static_cast<uint32_t>(
+          __builtin_amdgcn_readfirstlane(static_cast<int>(lds_ld(kLdsWork)))));
+#else
+      const uint32_t at = ue;
+#endif
+      const uint32_t est = ws.units > at ? ws.units - at : 0u;
+      uint32_t want = est / (WIPDB_GUIDE * kSpansPerWG);
       want = want < 1u ? 1u : (want > static_cast<uint32_t>(G) ? static_cast<uint32_t>(G) : want);
       uint32_t old = 0u;
       if (lane == static_cast<uint32_t>(g * G))
