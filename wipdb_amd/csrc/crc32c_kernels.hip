@@ -100,6 +100,15 @@
 #ifndef WIPDB_DYN
 #define WIPDB_DYN 1
 #endif
+// WIPDB_GPOOL: workgroups start with a static share and then take 32-span
+// blocks from a grid-wide pool (global counter, LDS ring per workgroup), so
+// the XCDs that the fabric serves faster take more of the batch
+#ifndef WIPDB_GPOOL
+#define WIPDB_GPOOL 1
+#endif
+#if WIPDB_GPOOL && !WIPDB_DYN
+#error "WIPDB_GPOOL feeds the work-sharing cursor (WIPDB_DYN)"
+#endif
 // WIPDB_GUIDE: guided batch = what is left / (WIPDB_GUIDE * groups sharing);
 // WIPDB_FRESH_EST: read the counter for that instead of the group's last grab
 #ifndef WIPDB_GUIDE
@@ -333,12 +342,14 @@ struct DescSource {
                    // (masked) crc, read at fetch time; the CRC starts at 0
   uint64_t c_off;  // per lane
   uint32_t c_len, c_init;
+  uint32_t c_span;  // WIPDB_GPOOL: the span index of the lane's entry
   uint32_t cj[S];  // next cache index per group (uniform)
 
   __device__ __forceinline__ void reset() {
     c_off = 0;
     c_len = 0;
     c_init = 0;
+    c_span = 0;
 #pragma unroll
     for (int g = 0; g < S; ++g) cj[g] = G;
   }
@@ -364,7 +375,8 @@ struct DescSource {
                                               uint32_t lane) {
     const uint32_t j = lane & (G - 1);
     if ((lane / G) == static_cast<uint32_t>(g) && j < nb) {
-      const uint64_t sp = ws.span_of(ub + j);
+      const uint64_t sp = ws.span_of_lane(ub + j);
+      c_span = static_cast<uint32_t>(sp);
       c_off = __builtin_nontemporal_load(offsets + sp);
       c_len = __builtin_nontemporal_load(lengths + sp) + extra;
       if (trailer) {
@@ -375,6 +387,10 @@ struct DescSource {
         c_init = inits ? __builtin_nontemporal_load(inits + sp) : 0u;
       }
     }
+  }
+  // The span index of entry j of group g's batch (WIPDB_GPOOL).
+  __device__ __forceinline__ uint32_t span_at(int g, uint32_t j) const {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(c_span, g * G + j));
   }
   // Entry j of group g's batch (uniform j).
   __device__ __forceinline__ void at(int g, uint32_t j, uint64_t, uint64_t& start, uint32_t& len,
@@ -411,7 +427,11 @@ struct StridedSource {
   uint32_t init;
   uint64_t count;
   static constexpr bool trailer = false;
-  __device__ __forceinline__ void reset() {}
+  uint32_t c_span;  // WIPDB_GPOOL: per lane, the span index of the batch entry
+  __device__ __forceinline__ void reset() { c_span = 0; }
+  __device__ __forceinline__ uint32_t span_at(int g, uint32_t j) const {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(c_span, g * G + j));
+  }
   __device__ __forceinline__ void desc(int, uint64_t s, uint64_t, uint32_t, uint64_t& start,
                                        uint32_t& len, uint32_t& ini) const {
     start = reinterpret_cast<uint64_t>(base) + s * stride_bytes;
@@ -419,7 +439,16 @@ struct StridedSource {
     ini = init;
   }
   template <typename WS>
-  __device__ __forceinline__ void fetch_units(int, uint32_t, uint32_t, const WS&, uint32_t) {}
+  __device__ __forceinline__ void fetch_units(int g, uint32_t ub, uint32_t nb, const WS& ws,
+                                              uint32_t lane) {
+#if WIPDB_GPOOL
+    const uint32_t j = lane & (G - 1);
+    if ((lane / G) == static_cast<uint32_t>(g) && j < nb)
+      c_span = static_cast<uint32_t>(ws.span_of_lane(ub + j));
+#else
+    (void)g, (void)ub, (void)nb, (void)ws, (void)lane;
+#endif
+  }
   __device__ __forceinline__ void at(int, uint32_t, uint64_t s, uint64_t& start, uint32_t& len,
                                      uint32_t& ini) const {
     start = reinterpret_cast<uint64_t>(base) + s * stride_bytes;
@@ -434,24 +463,152 @@ struct StridedSource {
 // guided batches (half the per-group share of what is left, at most a
 // descriptor load's 32, at least 1), so a group that the SIMD's arbitration
 // serves faster simply takes more spans and all finish together.
+#if WIPDB_GPOOL
+// Grid-wide work pool (WIPDB_GPOOL).  The batch is cut into blocks of 32
+// consecutive spans.  Workgroup w starts with its static share, blocks
+// r * nwg + w for r < kStaticRounds (enough for each of its 32 groups'
+// first batch), and then takes blocks from the pool -- one global counter,
+// blocks kStaticRounds * nwg on -- into a ring in its LDS whenever fewer than
+// kAhead fetched units are left; unit u of the workgroup is span
+// ring[u / 32] * 32 + u % 32.  Its groups take units from the LDS counter in
+// guided batches as before.  One global atomic per pool grab -- ~50 per
+// microsecond for the whole chip at most, under the ~88 that one address
+// sustains (scripts/atomic_probe.hip) -- lets every CU finish within about
+// a span of the others, where static shares left the odd XCDs ~5 % behind.
+// A unit's ring entry is read once, when its batch is fetched (the span
+// index then rides in the descriptor cache, c_span): between a batch's
+// first unit and the newest fetched unit lie at most the batch, what the
+// other groups grab meanwhile (one batch each), kAhead and one pool grab --
+// fewer than the kRing blocks after which an entry is recycled.  (Spans are
+// 32-bit indices: count < 2^32 per launch.)
+constexpr uint32_t kRing = 64;          // block indices in the LDS ring
+constexpr uint32_t kStaticRounds = 32;  // a workgroup's static blocks
+constexpr uint32_t kAhead = 64;         // fetched units kept ahead of the counter
+constexpr uint32_t kMaxGrab = 4;        // blocks per pool grab
+constexpr uint32_t kPoolArrive = 32;    // u32 index of the arrival count (own 128-B line)
+static_assert(kRing * 32u > kSpansPerWG * G + G + kAhead + kMaxGrab * 32u,
+              "a batch's ring entries outlive its fetch");
+typedef __attribute__((address_space(3))) uint32_t l_u32w;
+// LDS words: the unit counter, units fetched, refill lock, pool exhausted,
+// this workgroup's view of the pool position; then the ring
+__device__ __forceinline__ l_u32w* lw(uint32_t i) {
+  return reinterpret_cast<l_u32w*>(static_cast<uintptr_t>(kLdsWork + 4u * i));
+}
+enum : uint32_t { kWCtr = 0, kWAvail = 1, kWLock = 2, kWDone = 3, kWPos = 4, kWRing = 8 };
+static_assert(kLdsWork + 4u * (kWRing + kRing) <= kLdsMain, "pool state fits below the tables");
+
+// An LDS word, read by every lane, as a scalar.
+__device__ __forceinline__ uint32_t lds_word(uint32_t w) {
+  return uni(static_cast<uint32_t>(
+      __builtin_amdgcn_readfirstlane(static_cast<int>(__atomic_load_n(lw(w), __ATOMIC_ACQUIRE)))));
+}
+#endif
+
+// A workgroup's share of the batch: unit u is span (u / 32) * stride + wg0 +
+// u % 32 (or, with WIPDB_GPOOL, span ring[u / 32] * 32 + u % 32), and its
+// groups take units from an LDS counter in guided batches.
 struct WorkShare {
   uint64_t stride;  // spans per round of the grid (groups in the grid)
   uint64_t wg0;     // this workgroup's first span
-  uint32_t units;   // units of this workgroup
+  uint32_t units;   // units of this workgroup (WIPDB_GPOOL: unused)
+#if WIPDB_GPOOL
+  uint64_t count;
+  uint32_t nblk, nwg, first_pool;
+  uint32_t* pool;  // [0] the pool counter, [kPoolArrive] arrivals (release_pool)
+#endif
   __device__ __forceinline__ uint64_t span_of(uint32_t u) const {
+#if WIPDB_GPOOL
+    return static_cast<uint64_t>(lds_word(kWRing + ((u >> 5) & (kRing - 1u)))) * 32u + (u & 31u);
+#else
     return static_cast<uint64_t>(u >> 5) * stride + wg0 + (u & 31u);
+#endif
   }
-  __device__ __forceinline__ void init(uint64_t count) {
+  // The same for a per-lane unit (descriptor fetch).
+  __device__ __forceinline__ uint64_t span_of_lane(uint32_t u) const {
+#if WIPDB_GPOOL
+    return static_cast<uint64_t>(
+               __atomic_load_n(lw(kWRing + ((u >> 5) & (kRing - 1u))), __ATOMIC_RELAXED)) *
+               32u + (u & 31u);
+#else
+    return span_of(u);
+#endif
+  }
+  __device__ __forceinline__ void init(uint64_t n, uint32_t* p) {
     stride = grid_groups();
     wg0 = static_cast<uint64_t>(blockIdx.x) * kSpansPerWG;
     units = 0u;
-    if (count > wg0) {
-      const uint64_t r = count - wg0;
+#if WIPDB_GPOOL
+    // thread 0 sets up the LDS state; the caller's barrier publishes it.
+    // The last block may be short: `avail` then stops at the batch's end.
+    count = n;
+    pool = p;
+    nwg = gridDim.x;
+    nblk = static_cast<uint32_t>((n + 31u) >> 5);
+    first_pool = kStaticRounds * nwg;
+    if (threadIdx.x == 0u) {
+      uint32_t k = 0, av = 0;
+      for (; k < kStaticRounds && k * nwg + blockIdx.x < nblk; ++k) {
+        const uint32_t b = k * nwg + blockIdx.x;
+        *lw(kWRing + k) = b;
+        av = 32u * k + (b + 1u == nblk ? static_cast<uint32_t>(n - 32ull * b) : 32u);
+      }
+      *lw(kWCtr) = 0u;
+      *lw(kWAvail) = av;
+      *lw(kWLock) = 0u;
+      *lw(kWDone) = first_pool < nblk ? 0u : 1u;
+      *lw(kWPos) = 0u;
+    }
+#else
+    (void)p;
+    if (n > wg0) {
+      const uint64_t r = n - wg0;
       const uint64_t full = r / stride;
       const uint64_t part = r - full * stride;
       units = static_cast<uint32_t>(full * kSpansPerWG + (part < kSpansPerWG ? part : kSpansPerWG));
     }
+#endif
   }
+#if WIPDB_GPOOL
+  __device__ __forceinline__ uint32_t pool_left(uint32_t pos) const {
+    return nblk > first_pool + pos ? nblk - first_pool - pos : 0u;
+  }
+  // Take blocks from the pool into the ring, unless another group is doing
+  // so.  Uniform control flow: lane `ld` alone does the atomics and stores.
+  __device__ __forceinline__ void refill(uint32_t lane, uint32_t ld) const {
+    uint32_t busy = 1u;
+    if (lane == ld) {
+      uint32_t expect = 0u;
+      busy = __atomic_compare_exchange_n(lw(kWLock), &expect, 1u, false, __ATOMIC_ACQUIRE,
+                                         __ATOMIC_RELAXED)
+                 ? 0u
+                 : 1u;
+    }
+    if (uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(busy, ld))) != 0u) return;
+    if (lds_word(kWDone) == 0u) {
+      uint32_t nb = pool_left(lds_word(kWPos)) / (WIPDB_GUIDE * nwg);
+      nb = nb < 1u ? 1u : (nb > kMaxGrab ? kMaxGrab : nb);
+      uint32_t p = 0u;
+      if (lane == ld)
+        p = __hip_atomic_fetch_add(pool, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      p = uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(p, ld)));
+      const uint32_t b0 = first_pool + p;
+      const uint32_t nv = b0 < nblk ? (nblk - b0 < nb ? nblk - b0 : nb) : 0u;
+      const uint32_t av = lds_word(kWAvail);  // a multiple of 32 while blocks remain
+      const uint32_t i = lane - ld;
+      if (i < nv) *lw(kWRing + (((av >> 5) + i) & (kRing - 1u))) = b0 + i;
+      // the batch's last block may be short
+      const uint32_t add = nv == 0u ? 0u
+                           : (b0 + nv == nblk ? 32u * (nv - 1u) + static_cast<uint32_t>(count - 32ull * (nblk - 1u))
+                                              : 32u * nv);
+      if (lane == ld) {
+        __atomic_store_n(lw(kWPos), p + nb, __ATOMIC_RELAXED);
+        __atomic_store_n(lw(kWAvail), av + add, __ATOMIC_RELEASE);
+        if (nv < nb || b0 + nv == nblk) __atomic_store_n(lw(kWDone), 1u, __ATOMIC_RELEASE);
+      }
+    }
+    if (lane == ld) __atomic_store_n(lw(kWLock), 0u, __ATOMIC_RELEASE);
+  }
+#endif
   static __device__ __forceinline__ uint64_t grid_groups() {
     return static_cast<uint64_t>(gridDim.x) * kSpansPerWG;
   }
@@ -537,22 +694,31 @@ struct DynCursor {
   uint32_t rest, init, first, left;  // left: 1 while the group has a current span
   uint32_t u, ub, ue;                // current unit; grabbed batch [ub, ue)
   uint32_t split;                    // kFlagSkipSmall | kFlagSplitRem
+#if WIPDB_GPOOL
+  uint32_t span;                     // the current span (the ring entry may be recycled)
+#endif
   bool skip;
 
   // Makes unit u (the next one) current, grabbing a batch when needed.
   __device__ __forceinline__ void load(Src& src, int g, const WorkShare& ws, uint32_t lane) {
     if (u >= ue) {
+#if WIPDB_GPOOL
+      const uint32_t ld = static_cast<uint32_t>(g * G);
+      const uint32_t c = lds_word(kWCtr);
+      const uint32_t av0 = lds_word(kWAvail);
+      const uint32_t est =
+          (av0 > c ? av0 - c : 0u) + ws.pool_left(lds_word(kWPos)) * 32u / ws.nwg;
+#elif WIPDB_FRESH_EST
       // guided: a fraction of this group's share of what is left, read
       // from the counter just before the grab (other groups may take some
       // in between: the batch only comes out larger than the rule by what
       // they took)
-#if WIPDB_FRESH_EST
       const uint32_t at = uni(static_cast<uint32_t>(
           __builtin_amdgcn_readfirstlane(static_cast<int>(lds_ld(kLdsWork)))));
-#else
-      const uint32_t at = ue;
-#endif
       const uint32_t est = ws.units > at ? ws.units - at : 0u;
+#else
+      const uint32_t est = ws.units > ue ? ws.units - ue : 0u;
+#endif
       uint32_t want = est / (WIPDB_GUIDE * kSpansPerWG);
       want = want < 1u ? 1u : (want > static_cast<uint32_t>(G) ? static_cast<uint32_t>(G) : want);
       uint32_t old = 0u;
@@ -562,18 +728,43 @@ struct DynCursor {
                 static_cast<uintptr_t>(kLdsWork)),
             want, __ATOMIC_RELAXED);
       old = uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(old, g * G)));
-      if (old >= ws.units) {
+#if WIPDB_GPOOL
+      // wait until the batch is fetched or the pool is empty, refilling
+      // ahead (bounded: a refill is one global atomic away)
+      const uint32_t end = old + want;
+      uint32_t av = 0u;
+      for (uint32_t it = 0; it < (1u << 22); ++it) {
+        const uint32_t dn = lds_word(kWDone);
+        av = lds_word(kWAvail);
+        if (dn == 0u && av < end + kAhead) ws.refill(lane, ld);
+        if (av >= end) break;
+        if (dn != 0u) {
+          av = lds_word(kWAvail);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const uint32_t lim = av < end ? av : end;
+#else
+      const uint32_t lim = old + want < ws.units ? old + want : ws.units;
+#endif
+      if (old >= lim) {
         left = 0u;
-        ue = ws.units;
+        ue = lim;
         return;
       }
       ub = old;
-      ue = old + want < ws.units ? old + want : ws.units;
+      ue = lim;
       u = ub;
       src.fetch_units(g, ub, ue - ub, ws, lane);
     }
     left = 1u;
+#if WIPDB_GPOOL
+    span = src.span_at(g, u - ub);
+    src.at(g, u - ub, span, start, rest, init);
+#else
     src.at(g, u - ub, ws.span_of(u), start, rest, init);
+#endif
   }
   __device__ __forceinline__ void skip_small(Src& src, int g, const WorkShare& ws, uint32_t lane) {
     while (skip && left != 0u && rest <= kSmallMax) {
@@ -607,7 +798,11 @@ struct DynCursor {
     sl.init = init;
     sl.meta = n | ((kSlotValid | (first ? kSlotFirst : 0u) | (last ? kSlotLast : 0u) |
                     (cut ? kSlotPartial : 0u)) << 16);
+#if WIPDB_GPOOL
+    sl.ord = span;
+#else
     sl.ord = u;
+#endif
     if (last) {
       first = 1u;
       ++u;
@@ -1002,7 +1197,8 @@ __device__ __forceinline__ void process_seg(const Slot (&s)[S], u32x4 (&d)[NLT],
 // and crc uniform).
 template <typename Src, typename Emit>
 __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t waves,
-                                          const void* dummy, uint32_t split, Emit emit) {
+                                          const void* dummy, uint32_t split, uint32_t* work,
+                                          Emit emit) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l4 = (threadIdx.x & 31u) * 4u;
   const uint32_t s0 = l4 | ((l4 | 0x80u) << 8) | (1u << 24);
@@ -1011,9 +1207,14 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
   src.reset();
 #if WIPDB_DYN
   WorkShare ws;
-  ws.init(src.count);
-  DynCursor<Src> cur[S];
+  ws.init(src.count, work);
+#if WIPDB_GPOOL
+  __syncthreads();
+  auto span_of = [&](int, uint32_t ord) { return static_cast<uint64_t>(ord); };
+#else
   auto span_of = [&](int, uint32_t ord) { return ws.span_of(ord); };
+#endif
+  DynCursor<Src> cur[S];
 #else
   SegCursor<Src> cur[S];
   auto span_of = [&](int g, uint32_t ord) {
@@ -1145,6 +1346,27 @@ __device__ __forceinline__ uint64_t grid_waves() {
   return static_cast<uint64_t>(gridDim.x) * kWaves;
 }
 
+// End of a kernel that took blocks from the pool `work`: once all of a
+// workgroup's waves are done it checks in, and the last workgroup to check
+// in zeroes the pool counter and the arrival count, so the buffer is ready
+// for its next launch (hcrc_api.cc WorkPool).
+__device__ __forceinline__ void release_pool(uint32_t* work) {
+#if WIPDB_GPOOL
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    uint32_t* arrived = work + kPoolArrive;
+    const uint32_t n =
+        __hip_atomic_fetch_add(arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (n + 1u == gridDim.x) {
+      __hip_atomic_store(work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(arrived, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#else
+  (void)work;
+#endif
+}
+
 // Stores one value per finished span: lane g*G writes group g's result.
 __device__ __forceinline__ bool group_leader(int g) {
   return (threadIdx.x & 63u) == static_cast<uint32_t>(g * G);
@@ -1158,7 +1380,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags,
-    const DevTables* __restrict__ tab) {
+    const DevTables* __restrict__ tab, uint32_t* __restrict__ work) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
 #if WIPDB_TIMELINE
   const uint64_t t_entry = wall_clock64();
@@ -1172,9 +1394,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
     tl[1] = wall_clock64();
   }
 #endif
-  DescSource src{base, offsets, lengths, inits, count, 0u, false, 0, 0, 0, {0, 0}};
+  DescSource src{base, offsets, lengths, inits, count, 0u, false, 0, 0, 0, 0, {0, 0}};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, flags & (kFlagSkipSmall | kFlagSplitRem),
+  run_waves(src, wave_id(), grid_waves(), tab, flags & (kFlagSkipSmall | kFlagSplitRem), work,
             [&](uint64_t span, uint32_t crc, int g, uint32_t, bool partial) {
     // a partial CRC (remainder left to the small kernel) stays unmasked
     if (group_leader(g)) out[span] = msk && !partial ? mask_crc(crc) : crc;
@@ -1182,21 +1404,23 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
 #if WIPDB_TIMELINE
   if (stamp) tl[2 + (threadIdx.x >> 6)] = wall_clock64();
 #endif
+  release_pool(work);
 }
 
 // Fixed-size blocks at a fixed stride.
 __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
     const uint8_t* __restrict__ base, uint64_t stride_bytes, uint32_t length, uint32_t init,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags,
-    const DevTables* __restrict__ tab) {
+    const DevTables* __restrict__ tab, uint32_t* __restrict__ work) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
-  StridedSource src{base, stride_bytes, length, init, count};
+  StridedSource src{base, stride_bytes, length, init, count, 0u};
   const bool msk = (flags & kFlagMask) != 0;
-  run_waves(src, wave_id(), grid_waves(), tab, 0u,
+  run_waves(src, wave_id(), grid_waves(), tab, 0u, work,
             [&](uint64_t span, uint32_t crc, int g, uint32_t, bool) {
     if (group_leader(g)) out[span] = msk ? mask_crc(crc) : crc;
   });
+  release_pool(work);
 }
 
 // Read-side verify: block = base + off, n = handle size; crc over n+1 bytes
@@ -1204,19 +1428,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
 __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
-    const DevTables* __restrict__ tab) {
+    const DevTables* __restrict__ tab, uint32_t* __restrict__ work) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
   // the stored trailer crc rides in the descriptor cache (fetched with the
   // offsets, 32 spans at a time), so emitting a status needs no load
-  DescSource src{base, offsets, lengths, nullptr, count, 1u, true, 0, 0, 0, {0, 0}};
-  run_waves(src, wave_id(), grid_waves(), tab, 0u,
+  DescSource src{base, offsets, lengths, nullptr, count, 1u, true, 0, 0, 0, 0, {0, 0}};
+  run_waves(src, wave_id(), grid_waves(), tab, 0u, work,
             [&](uint64_t s, uint32_t crc, int g, uint32_t stored, bool) {
               if (group_leader(g)) {
                 const uint32_t rot = stored - 0xa282ead8u;
                 status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;
               }
             });
+  release_pool(work);
 }
 
 #include "crc32c_small.inc"

@@ -32,13 +32,13 @@ void Batch(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths
 namespace dev {
 __global__ void crc32c_spans_kernel(const uint8_t*, const uint64_t*,
                                     const uint32_t*, const uint32_t*, uint32_t*,
-                                    uint64_t, uint32_t, const DevTables*);
+                                    uint64_t, uint32_t, const DevTables*, uint32_t*);
 __global__ void crc32c_strided_kernel(const uint8_t*, uint64_t, uint32_t,
                                       uint32_t, uint32_t*, uint64_t, uint32_t,
-                                      const DevTables*);
+                                      const DevTables*, uint32_t*);
 __global__ void crc32c_verify_kernel(const uint8_t*, const uint64_t*,
                                      const uint32_t*, uint8_t*, uint64_t,
-                                     const DevTables*);
+                                     const DevTables*, uint32_t*);
 __global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*,
                                   uint64_t);
 __global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
@@ -76,7 +76,17 @@ struct Slot {
 
 }  // namespace
 
+// A launch's work-pool counters (crc32c_kernels.hip WorkShare, WIPDB_GPOOL):
+// the pool counter and the arrival count, 128 bytes apart.  The kernel's
+// last workgroup zeroes them, so a buffer is ready again once `ev`
+// (recorded after its launch) has completed.
+struct PoolBuf {
+  uint32_t* p = nullptr;
+  hipEvent_t ev = nullptr;
+};
+
 struct hcrc_ctx {
+  std::vector<PoolBuf> pools;  // under mu
   int device = -1;
   hipStream_t stream = nullptr;
   DevTables* d_tab = nullptr;
@@ -121,14 +131,59 @@ int LaunchGrid(hcrc_ctx* ctx, size_t count) {
   return static_cast<int>(std::max<size_t>(g, 1));
 }
 
+// A pool buffer no launch is using (caller holds ctx->mu); Release records
+// the launch that uses it.  Buffers are zeroed once at allocation, and every
+// launch leaves its buffer zeroed (release_pool), so reuse needs no memset.
+struct WorkPool {
+  hcrc_ctx* ctx = nullptr;
+  size_t idx = 0;
+  uint32_t* p = nullptr;
+  int Acquire(hcrc_ctx* c, hipStream_t st) {
+    ctx = c;
+    for (idx = 0; idx < ctx->pools.size(); ++idx)
+      if (hipEventQuery(ctx->pools[idx].ev) == hipSuccess) break;
+    if (idx == ctx->pools.size()) {
+      PoolBuf b;
+      HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&b.p), 256));
+      if (hipMemsetAsync(b.p, 0, 256, st) != hipSuccess ||
+          hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipFree(b.p);
+        return HCRC_ERR_HIP;
+      }
+      ctx->pools.push_back(b);
+    }
+    p = ctx->pools[idx].p;
+    return HCRC_OK;
+  }
+  int Release(hipStream_t st) {
+    if (!p) return HCRC_OK;
+    p = nullptr;
+    return hipEventRecord(ctx->pools[idx].ev, st) == hipSuccess ? HCRC_OK : HCRC_ERR_HIP;
+  }
+};
+
+// The kernels keep span indices in 32 bits: larger batches go in pieces.
+constexpr size_t kMaxLaunchSpans = size_t(1) << 31;
+
 int LaunchSpansKernel(hcrc_ctx* ctx, const void* base, const uint64_t* off,
                       const uint32_t* len, const uint32_t* init, uint32_t* out,
                       size_t count, uint32_t kflags, hipStream_t st) {
-  hipLaunchKernelGGL(wipdb::dev::crc32c_spans_kernel, dim3(LaunchGrid(ctx, count)),
-                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
-                     static_cast<const uint8_t*>(base), off, len, init, out,
-                     static_cast<uint64_t>(count), kflags, ctx->d_tab);
-  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+  for (size_t pos = 0; pos < count; pos += kMaxLaunchSpans) {
+    const size_t n = std::min(count - pos, kMaxLaunchSpans);
+    WorkPool wp;
+    int rc = wp.Acquire(ctx, st);
+    if (rc != HCRC_OK) return rc;
+    hipLaunchKernelGGL(wipdb::dev::crc32c_spans_kernel, dim3(LaunchGrid(ctx, n)),
+                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+                       static_cast<const uint8_t*>(base), off + pos, len + pos,
+                       init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n), kflags,
+                       ctx->d_tab, wp.p);
+    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+    const int rr = wp.Release(st);
+    if (rc == HCRC_OK) rc = rr;
+    if (rc != HCRC_OK) return rc;
+  }
+  return HCRC_OK;
 }
 
 // HCRC_SPLIT_SMALL: the spans of at most kSmallMax bytes are compacted by
@@ -515,6 +570,13 @@ int hcrc_ctx_destroy(hcrc_ctx* ctx) {
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.done) (void)hipEventDestroy(s.done);
   }
+  for (PoolBuf& b : ctx->pools) {
+    if (b.ev) {
+      (void)hipEventSynchronize(b.ev);
+      (void)hipEventDestroy(b.ev);
+    }
+    (void)hipFree(b.p);
+  }
   if (ctx->d_tab) (void)hipFree(ctx->d_tab);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -569,13 +631,23 @@ int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
   if (count == 0) return HCRC_OK;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HCRC_CHECK(hipSetDevice(ctx->device));
-  hipLaunchKernelGGL(wipdb::dev::crc32c_strided_kernel,
-                     dim3(LaunchGrid(ctx, count)), dim3(wipdb::dev::kThreads),
-                     wipdb::dev::kLdsBytes, StreamOf(ctx, stream),
-                     static_cast<const uint8_t*>(d_base), stride, length, init_crc,
-                     d_out_crcs, static_cast<uint64_t>(count),
-                     static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_tab);
-  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+  const hipStream_t st = StreamOf(ctx, stream);
+  for (size_t pos = 0; pos < count; pos += kMaxLaunchSpans) {
+    const size_t n = std::min(count - pos, kMaxLaunchSpans);
+    WorkPool wp;
+    int rc = wp.Acquire(ctx, st);
+    if (rc != HCRC_OK) return rc;
+    hipLaunchKernelGGL(wipdb::dev::crc32c_strided_kernel, dim3(LaunchGrid(ctx, n)),
+                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+                       static_cast<const uint8_t*>(d_base) + pos * stride, stride, length,
+                       init_crc, d_out_crcs + pos, static_cast<uint64_t>(n),
+                       static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_tab, wp.p);
+    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+    const int rr = wp.Release(st);
+    if (rc == HCRC_OK) rc = rr;
+    if (rc != HCRC_OK) return rc;
+  }
+  return HCRC_OK;
 }
 
 int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
@@ -587,12 +659,22 @@ int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offse
   if (count == 0) return HCRC_OK;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HCRC_CHECK(hipSetDevice(ctx->device));
-  hipLaunchKernelGGL(wipdb::dev::crc32c_verify_kernel, dim3(LaunchGrid(ctx, count)),
-                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes,
-                     StreamOf(ctx, stream), static_cast<const uint8_t*>(d_base),
-                     d_offsets, d_lengths, d_status, static_cast<uint64_t>(count),
-                     ctx->d_tab);
-  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+  const hipStream_t st = StreamOf(ctx, stream);
+  for (size_t pos = 0; pos < count; pos += kMaxLaunchSpans) {
+    const size_t n = std::min(count - pos, kMaxLaunchSpans);
+    WorkPool wp;
+    int rc = wp.Acquire(ctx, st);
+    if (rc != HCRC_OK) return rc;
+    hipLaunchKernelGGL(wipdb::dev::crc32c_verify_kernel, dim3(LaunchGrid(ctx, n)),
+                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+                       static_cast<const uint8_t*>(d_base), d_offsets + pos, d_lengths + pos,
+                       d_status + pos, static_cast<uint64_t>(n), ctx->d_tab, wp.p);
+    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+    const int rr = wp.Release(st);
+    if (rc == HCRC_OK) rc = rr;
+    if (rc != HCRC_OK) return rc;
+  }
+  return HCRC_OK;
 }
 
 int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
