@@ -241,6 +241,49 @@ def test_batch_counts_work_sharing(engine, oracle, count):
     np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
 
 
+@pytest.mark.parametrize("count", [262144, 262145, 262144 + 31, 262144 + 33, 300001, 1 << 20])
+def test_pool_counts(engine, oracle, count):
+    """Batches past the workgroups' static share (32 rounds x 256 CUs x 32
+    spans = 262144 spans) take blocks from the grid-wide pool: a short last
+    block, a pool of one block, a pool of many; short spans so the oracle
+    stays quick, at random offsets and with inits."""
+    rng = np.random.default_rng(count)
+    buf = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    lens = rng.integers(0, 200, count).astype(np.uint32)
+    offs = rng.integers(0, buf.size - 200, count).astype(np.uint64)
+    inits = rng.integers(0, 2**32, size=count, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
+
+
+def test_pool_buffers_across_streams_and_relaunches(engine, oracle):
+    """Pool counters are per launch: back-to-back launches on one stream and
+    concurrent launches on three streams (each large enough to use the pool)
+    all get every span right -- the kernel's last workgroup must leave each
+    buffer zeroed for its next launch."""
+    import torch
+    rng = np.random.default_rng(99)
+    buf = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    dbuf = torch.from_numpy(buf).cuda()
+    jobs = []
+    for k in range(9):
+        n = int(rng.integers(280000, 330000))
+        lens = rng.integers(0, 160, n).astype(np.uint32)
+        offs = rng.integers(0, buf.size - 160, n).astype(np.uint64)
+        jobs.append((torch.from_numpy(offs.view(np.int64)).cuda(),
+                     torch.from_numpy(lens.view(np.int32)).cuda(),
+                     oracle.batch(buf, offs, lens)))
+    torch.cuda.synchronize()  # the uploads happened on the current stream
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = []
+    for rep in range(2):
+        for k, (o, ln, _) in enumerate(jobs):
+            outs.append((k, engine.batch_device(dbuf, o, ln, stream=streams[k % 3])))
+    torch.cuda.synchronize()
+    for k, out in outs:
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), jobs[k][2])
+
+
 def test_zipf_mixed_sst_packing(engine, oracle):
     rng = np.random.default_rng(13)
     buckets = np.array([512, 1024, 2048, 4096, 8192, 16384, 32768, 65536])
