@@ -52,10 +52,13 @@
 //   WIPDB_CPC      16-byte chunks per chain (1 or 2)
 //   WIPDB_NT       nontemporal data loads (1) or plain (0)
 //   WIPDB_XCHG     C == 2 with coalesced loads + DPP pair exchange
-//   WIPDB_SLOTS    register-ring depth (2 or 3; 3 spills at K = 8)
+//   WIPDB_SLOTS    register-ring depth (1, 2 or 3; 3 spills at K = 8)
 //   WIPDB_ILP      chains interleaved per feed step
 //   WIPDB_LOADONLY diagnostic: the loads and ring without the CRC work
 //   WIPDB_NOFOLD   diagnostic: the scan without the cross-chain fold
+//   WIPDB_NO_TABLES, WIPDB_RS_UNROLL, WIPDB_RS_SPLIT: diagnostics for the
+//                  load-only skeleton and the read-stream kernel
+//                  (scripts/stream_probe.py)
 #ifndef WIPDB_NT
 #define WIPDB_NT 0
 #endif
@@ -108,6 +111,15 @@
 #endif
 #if WIPDB_GPOOL && !WIPDB_DYN
 #error "WIPDB_GPOOL feeds the work-sharing cursor (WIPDB_DYN)"
+#endif
+#ifndef WIPDB_RS_UNROLL
+#define WIPDB_RS_UNROLL 1
+#endif
+#ifndef WIPDB_RS_SPLIT
+#define WIPDB_RS_SPLIT 0
+#endif
+#ifndef WIPDB_NO_TABLES
+#define WIPDB_NO_TABLES 0
 #endif
 // WIPDB_GUIDE: guided batch = what is left / (WIPDB_GUIDE * groups sharing);
 // WIPDB_FRESH_EST: read the counter for that instead of the group's last grab
@@ -1268,7 +1280,18 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
              (sl[g].flags() & kSlotPartial) != 0u);
   };
 
-#if WIPDB_SLOTS == 3
+#if WIPDB_SLOTS == 1
+  // One slot: issue a segment pair's loads, wait for all of them, compute
+  // (nothing of this wave in flight while it computes).
+  Slot sA[S];
+  u32x4 bA[NLT];
+  for (;;) {
+    next(sA);
+    if (!valid(sA)) break;
+    issue_seg(sA, lane, dummy, bA);
+    finish(sA, bA);
+  }
+#elif WIPDB_SLOTS == 3
   // Three slots: while one pair is processed the next two pairs' loads are
   // in flight.
   Slot sA[S], sB[S], sC[S];
@@ -1316,6 +1339,11 @@ __device__ __forceinline__ void run_waves(Src& src, uint64_t wave, uint64_t wave
 // Copy the device tables into LDS: main tables replicated 32x, the rest
 // linear.  Every thread of the workgroup takes part; ends with a barrier.
 __device__ __forceinline__ void load_tables(uint8_t* lds, const DevTables* __restrict__ tab) {
+#if WIPDB_NO_TABLES  // diagnostic (load-only builds): skip the table copy
+  if (threadIdx.x == 0u) *reinterpret_cast<uint32_t*>(lds + kLdsWork) = 0u;
+  __syncthreads();
+  return;
+#endif
   const uint32_t tid = threadIdx.x;
   const uint32_t nthr = blockDim.x;
   // main: 4 tables x 256 bytes x 32 replicas; 4 consecutive replicas per store
@@ -1454,13 +1482,52 @@ __global__ __launch_bounds__(kThreads) void readstream_kernel(
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
   const uint32_t chunks = length >> 4;
+#if WIPDB_RS_SPLIT
+  // diagnostic: a half-wave per block, like the CRC kernels' lane groups
+  // (32 lanes x WIPDB_RS_UNROLL loads in flight)
+  for (uint64_t s2 = wave_id(); 2 * s2 < count; s2 += nw) {
+    const uint64_t s = 2 * s2 + (lane >> 5);
+    uint32_t acc = 0;
+    if (s < count) {
+      g_u32x4* cp = reinterpret_cast<g_u32x4*>(reinterpret_cast<uintptr_t>(base + s * stride));
+      uint32_t i = lane & 31u;
+      for (; i + 32u * (WIPDB_RS_UNROLL - 1) < chunks; i += 32u * WIPDB_RS_UNROLL) {
+        u32x4 v[WIPDB_RS_UNROLL];
+#pragma unroll
+        for (int k = 0; k < WIPDB_RS_UNROLL; ++k) v[k] = __builtin_nontemporal_load(cp + i + 32u * k);
+#pragma unroll
+        for (int k = 0; k < WIPDB_RS_UNROLL; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+      }
+    }
+#pragma unroll
+    for (int k = 16; k >= 1; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
+    if ((lane & 31u) == 0u && s < count) out[s] = acc;
+  }
+  return;
+#endif
   for (uint64_t s = wave_id(); s < count; s += nw) {
     g_u32x4* cp = reinterpret_cast<g_u32x4*>(reinterpret_cast<uintptr_t>(base + s * stride));
     uint32_t acc = 0;
+#if WIPDB_RS_UNROLL > 1
+    // diagnostic: more loads in flight per wave
+    uint32_t i = lane;
+    for (; i + 64u * (WIPDB_RS_UNROLL - 1) < chunks; i += 64u * WIPDB_RS_UNROLL) {
+      u32x4 v[WIPDB_RS_UNROLL];
+#pragma unroll
+      for (int k = 0; k < WIPDB_RS_UNROLL; ++k) v[k] = __builtin_nontemporal_load(cp + i + 64u * k);
+#pragma unroll
+      for (int k = 0; k < WIPDB_RS_UNROLL; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < chunks; i += 64) {
+      const u32x4 v = __builtin_nontemporal_load(cp + i);
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+#else
     for (uint32_t i = lane; i < chunks; i += 64) {
       const u32x4 v = __builtin_nontemporal_load(cp + i);
       acc ^= v.x ^ v.y ^ v.z ^ v.w;
     }
+#endif
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
     if (lane == 0) out[s] = acc;

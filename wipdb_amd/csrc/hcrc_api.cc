@@ -538,6 +538,9 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
   HCRC_CHECK(hipFuncSetAttribute(
       reinterpret_cast<const void*>(wipdb::dev::crc32c_small_kernel),
       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::dev::readstream_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   std::unique_ptr<DevTables> ht(new DevTables);
   BuildDevTables(ht.get());
   HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_tab), sizeof(DevTables)));
@@ -686,8 +689,12 @@ int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
   std::lock_guard<std::mutex> lk(ctx->mu);
   HCRC_CHECK(hipSetDevice(ctx->device));
   // same geometry as the CRC kernels, no LDS tables
+#ifndef WIPDB_RS_LDS
+#define WIPDB_RS_LDS 0
+#endif
   hipLaunchKernelGGL(wipdb::dev::readstream_kernel, dim3(LaunchGrid(ctx, count)),
-                     dim3(wipdb::dev::kThreads), 0, StreamOf(ctx, stream),
+                     dim3(wipdb::dev::kThreads), WIPDB_RS_LDS ? wipdb::dev::kLdsBytes : 0,
+                     StreamOf(ctx, stream),
                      static_cast<const uint8_t*>(d_base), stride, length, d_out,
                      static_cast<uint64_t>(count));
   return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
