@@ -118,6 +118,9 @@
 #ifndef WIPDB_RS_SPLIT
 #define WIPDB_RS_SPLIT 0
 #endif
+#ifndef WIPDB_RS_SALU
+#define WIPDB_RS_SALU 0
+#endif
 #ifndef WIPDB_NO_TABLES
 #define WIPDB_NO_TABLES 0
 #endif
@@ -1499,6 +1502,15 @@ __global__ __launch_bounds__(kThreads) void readstream_kernel(
         for (int k = 0; k < WIPDB_RS_UNROLL; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
       }
     }
+#if WIPDB_RS_SALU
+    // diagnostic: the CRC skeleton's scalar work per slot, as dependent SALU ops
+    {
+      uint32_t x = static_cast<uint32_t>(s2);
+#pragma unroll
+      for (int k = 0; k < WIPDB_RS_SALU; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(x));
+      acc ^= x & 0x80000000u;
+    }
+#endif
 #pragma unroll
     for (int k = 16; k >= 1; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
     if ((lane & 31u) == 0u && s < count) out[s] = acc;
