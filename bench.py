@@ -46,7 +46,7 @@ SEED = 0x4B10C5
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=50)  # >= 50 back-to-back launches
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
     p.add_argument("--mode", choices=["spans", "strided"], default="spans")
