@@ -17,7 +17,7 @@
  *       leveldb/util/crc32c.cc:275) is the same function.
  *   hcrc_batch_strided_async
  *       the same for fixed-size, fixed-stride blocks (no descriptor arrays).
- *   hcrc_verify_async
+ *   hcrc_verify_async, hcrc_verify_async_ex
  *       ReadBlock's check (kv/src/table/format.cc:91-99):
  *       Unmask(stored) == Value(data, n+1) for a batch of blocks.
  *   hcrc_batch_multi
@@ -125,6 +125,13 @@ int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base,
 int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base,
                       const uint64_t* d_offsets, const uint32_t* d_lengths,
                       uint8_t* d_status, size_t count, void* stream);
+/* The same with flags: 0 or HCRC_SPLIT_SMALL (blocks of at most 1 KiB, and
+ * the last 16..1024 bytes of blocks that just overrun 4 KiB -- a table's
+ * data blocks are 4 KiB plus their last entry -- go to the small-span
+ * kernel).  count < 2^31 per call with HCRC_SPLIT_SMALL. */
+int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base,
+                         const uint64_t* d_offsets, const uint32_t* d_lengths,
+                         uint8_t* d_status, size_t count, int flags, void* stream);
 
 /* Wait for all work on `stream` (NULL = the HIP default stream). */
 int hcrc_sync(hcrc_ctx* ctx, void* stream);

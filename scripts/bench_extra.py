@@ -176,6 +176,39 @@ def run_verify(eng, d, stream, rng, nblk=1 << 20):
             "kernel_ms": round(t * 1e3, 4), "corrupted": 64, "flagged": flagged}
 
 
+def run_vtblocks(eng, d, stream, rng, gib=4.0):
+    """Read side on table-block-shaped data: 4096..4224-byte blocks + type
+    byte + masked crc, SST-packed, device-resident; verify without and with
+    HCRC_SPLIT_SMALL."""
+    nbytes = int(gib * 2**30)
+    n = nbytes // 4165
+    lens = rng.integers(4096, 4225, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 5)[:-1]]).astype(np.uint64)
+    size = (int(offs[-1]) + int(lens[-1]) + 5 + 8191) // 4096 * 4096
+    data = torch.empty(size, dtype=torch.uint8, device=d)
+    eng.fill_splitmix64_device(data, 13, stream=stream.cuda_stream)
+    do, dl = dev(offs, d), dev(lens, d)
+    crc = eng.batch_device(data, do, dev(lens + 1, d), mask_output=True, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    # stamp the trailers (byte n+1..n+4 of every block)
+    pos = torch.from_numpy((offs + lens + 1).astype(np.int64)).to(d)
+    cb = crc.view(torch.uint8).view(n, 4)
+    for k in range(4):
+        data[pos + k] = cb[:, k]
+    torch.cuda.synchronize()
+    res = {"config": "read side: verify of table blocks 4096..4224 B + type + crc, SST-packed",
+           "blocks": int(n), "bytes": int((lens + 1).sum())}
+    for split in (False, True):
+        st = torch.empty(n, dtype=torch.uint8, device=d)
+        t = time_kernel(lambda: eng.verify_device(data, do, dl, st, stream=stream.cuda_stream,
+                                                  split_small=split), stream, 10)
+        res["split" if split else "verify_kernel"] = {
+            "GiBps": round(float((lens + 1).sum()) / t / 2**30, 1), "ms": round(t * 1e3, 4),
+            "all_ok": bool((st == 1).all())}
+    del data
+    return res
+
+
 def sst_layout(rng, n_sst):
     """8Binsert-shaped SSTs (test_bench/8Binsert.sh): spans cover contents +
     type byte; every block is followed by its 4-byte crc slot."""
@@ -249,6 +282,8 @@ def main():
                 r = run_verify(eng, d, stream, rng)
             elif w == "tblocks":
                 r = run_tblocks(eng, d, stream, rng)
+            elif w == "vtblocks":
+                r = run_vtblocks(eng, d, stream, rng)
             elif w == "sst":
                 r = run_sst(eng, rng, a.ssts)
             elif w == "host4k":

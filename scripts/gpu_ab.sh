@@ -18,6 +18,9 @@ for r in 1 2; do for v in $VARIANTS; do
   case ",$EXTRA," in *,tblocks,*)
     timeout -k 10 300 python scripts/bench_extra.py --what tblocks > gpurun_out/tb.txt 2>&1 || exit 1
     echo "$v tblocks $(grep '^{' gpurun_out/tb.txt | cut -c1-400)";; esac
+  case ",$EXTRA," in *,vtblocks,*)
+    timeout -k 10 300 python scripts/bench_extra.py --what vtblocks > gpurun_out/vtb.txt 2>&1 || exit 1
+    echo "$v vtblocks $(grep '^{' gpurun_out/vtb.txt | cut -c1-400)";; esac
   case ",$EXTRA," in *,mixed,*)
     timeout -k 10 300 python scripts/bench_extra.py --what mixed > gpurun_out/mx.txt 2>&1 || exit 1
     echo "$v mixed $(python - <<'PY'

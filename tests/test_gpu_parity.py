@@ -380,6 +380,55 @@ def test_verify_blocks(engine, oracle):
     expect = np.ones(offs.size, np.uint8)
     expect[bad] = 0
     np.testing.assert_array_equal(status, expect)
+    # HCRC_SPLIT_SMALL: the remainders after the first segment go to the
+    # small kernel (which reads the trailer itself)
+    st2 = engine.verify_device(_t(buf), _t(offs), _t(lens), split_small=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st2.cpu().numpy(), expect)
+
+
+def test_verify_split_every_size_class(engine, oracle):
+    """Verify with HCRC_SPLIT_SMALL over blocks of 0..1100 bytes (small
+    kernel), 1100..4110 (spans kernel, one segment), 4111..5125 (cut after
+    the first segment, remainder on the small kernel) and 5126..9000 (two
+    segments), SST-packed at every alignment, with corruptions in the
+    contents' first segment, in the remainder, in the type byte and in the
+    trailer."""
+    import torch
+    rng = np.random.default_rng(23)
+    buf = np.zeros(24 << 20, np.uint8)
+    offs, lens, cur = [], [], 0
+    classes = [(0, 1100), (1100, 4110), (4111, 5126), (5126, 9000)]
+    while True:
+        lo, hi = classes[len(offs) % 4]
+        n = int(rng.integers(lo, hi))
+        if cur + n + 5 >= buf.size:
+            break
+        buf[cur:cur + n] = rng.integers(0, 256, n, dtype=np.uint8)
+        buf[cur + n] = len(offs) & 1
+        offs.append(cur)
+        lens.append(n)
+        cur += n + 5
+    offs, lens = np.array(offs, np.uint64), np.array(lens, np.uint32)
+    crcs = oracle.batch(buf, offs, lens + 1)
+    for o, n, c in zip(offs, lens, crcs):
+        m = int(oracle.lib.oracle_mask(int(c)))
+        buf[int(o) + int(n) + 1:int(o) + int(n) + 5] = np.frombuffer(m.to_bytes(4, "little"), np.uint8)
+    bad = rng.choice(offs.size, 200, replace=False)
+    for i, b in enumerate(bad):
+        o, n = int(offs[b]), int(lens[b])
+        where = [o + (int(rng.integers(0, n)) if n else n),      # contents (first part)
+                 o + max(0, n - int(rng.integers(1, 16))) if n else o + n,  # near the end
+                 o + n,                                           # type byte
+                 o + n + 1 + int(rng.integers(0, 4))][i % 4]      # trailer
+        buf[where] ^= 0x5A
+    expect = np.ones(offs.size, np.uint8)
+    expect[bad] = 0
+    dbuf, doffs, dlens = _t(buf), _t(offs), _t(lens)
+    for split in (False, True):
+        st = engine.verify_device(dbuf, doffs, dlens, split_small=split)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(st.cpu().numpy(), expect)
 
 
 def test_batch_multi_one_device(oracle, golden_spans):

@@ -50,6 +50,7 @@ _PROTOS = {
     "hcrc_batch_strided_async": (
         _c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint32, _c.c_uint32, _vp, _sz, _c.c_int, _vp]),
     "hcrc_verify_async": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "hcrc_verify_async_ex": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _c.c_int, _vp]),
     "hcrc_sync": (_c.c_int, [_vp, _vp]),
     "hcrc_batch_multi": (
         _c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _vp, _vp, _vp, _vp, _vp, _sz, _c.c_int]),

@@ -176,16 +176,21 @@ class Engine:
               "hcrc_batch_strided_async")
         return out_t
 
-    def verify_device(self, base_t, offsets_t, lengths_t, status_t=None, stream=None):
+    def verify_device(self, base_t, offsets_t, lengths_t, status_t=None, stream=None,
+                      split_small: bool = False):
         """ReadBlock's check on device blocks: status[i] = 1 iff the stored
-        masked crc at byte n+1 matches Value(block, n+1)."""
+        masked crc at byte n+1 matches Value(block, n+1).  ``split_small``:
+        HCRC_SPLIT_SMALL (small blocks and table-block remainders on the
+        small-span kernel)."""
         import torch
         n = int(offsets_t.numel())
         if status_t is None:
             status_t = torch.empty(n, dtype=torch.uint8, device=base_t.device)
-        check(self._lib.hcrc_verify_async(self._ctx, _ptr(base_t), _ptr(offsets_t), _ptr(lengths_t),
-                                          _ptr(status_t), n, self._stream_of(stream)),
-              "hcrc_verify_async")
+        check(self._lib.hcrc_verify_async_ex(self._ctx, _ptr(base_t), _ptr(offsets_t),
+                                             _ptr(lengths_t), _ptr(status_t), n,
+                                             HCRC_SPLIT_SMALL if split_small else 0,
+                                             self._stream_of(stream)),
+              "hcrc_verify_async_ex")
         return status_t
 
     def readstream_device(self, base_t, stride: int, length: int, count: int, out_t=None,

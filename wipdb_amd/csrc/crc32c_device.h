@@ -23,6 +23,9 @@ constexpr uint32_t kSmallMax = 1024;
 constexpr uint32_t kFlagSplitRem = 0x8;
 // small-span list entries that continue a span from out[id] (remainders)
 constexpr uint32_t kSmallIdRem = 0x80000000u;
+// small-span kernel, read-side verify: compare with the stored trailer
+// (LE32 right after the span) and write a status byte instead of a CRC
+constexpr uint32_t kFlagVerify = 0x10;
 
 // The remainder rule, shared by the spans kernel's cursor and the partition
 // kernel: a span of n bytes starting at address a is cut after its first

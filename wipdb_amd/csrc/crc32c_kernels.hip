@@ -1456,20 +1456,29 @@ __global__ __launch_bounds__(kThreads) void crc32c_strided_kernel(
 
 // Read-side verify: block = base + off, n = handle size; crc over n+1 bytes
 // compared with Unmask(LE32 at n+1) (kv/src/table/format.cc:91-99).
+// With HCRC_SPLIT_SMALL (flags kFlagSkipSmall | kFlagSplitRem) blocks of at
+// most kSmallMax bytes are left to the small kernel, and a block that just
+// overruns a segment stops after it, its partial CRC going to partial[s]
+// for the small kernel to continue (and to verify).
 __global__ __launch_bounds__(kThreads) void crc32c_verify_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
-    const DevTables* __restrict__ tab, uint32_t* __restrict__ work) {
+    const DevTables* __restrict__ tab, uint32_t* __restrict__ work, uint32_t flags,
+    uint32_t* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_tables(lds, tab);
   // the stored trailer crc rides in the descriptor cache (fetched with the
   // offsets, 32 spans at a time), so emitting a status needs no load
   DescSource src{base, offsets, lengths, nullptr, count, 1u, true, 0, 0, 0, 0, {0, 0}};
-  run_waves(src, wave_id(), grid_waves(), tab, 0u, work,
-            [&](uint64_t s, uint32_t crc, int g, uint32_t stored, bool) {
+  run_waves(src, wave_id(), grid_waves(), tab, flags & (kFlagSkipSmall | kFlagSplitRem), work,
+            [&](uint64_t s, uint32_t crc, int g, uint32_t stored, bool cut) {
               if (group_leader(g)) {
-                const uint32_t rot = stored - 0xa282ead8u;
-                status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;
+                if (cut) {
+                  partial[s] = crc;
+                } else {
+                  const uint32_t rot = stored - 0xa282ead8u;
+                  status[s] = ((rot >> 17) | (rot << 15)) == crc ? 1 : 0;
+                }
               }
             });
   release_pool(work);

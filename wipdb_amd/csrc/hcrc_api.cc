@@ -38,14 +38,14 @@ __global__ void crc32c_strided_kernel(const uint8_t*, uint64_t, uint32_t,
                                       const DevTables*, uint32_t*);
 __global__ void crc32c_verify_kernel(const uint8_t*, const uint64_t*,
                                      const uint32_t*, uint8_t*, uint64_t,
-                                     const DevTables*, uint32_t*);
+                                     const DevTables*, uint32_t*, uint32_t, uint32_t*);
 __global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*,
                                   uint64_t);
 __global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
 __global__ void crc32c_partition_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
-                                        const uint32_t*, uint64_t, SmallList);
+                                        const uint32_t*, uint64_t, SmallList, uint32_t);
 __global__ void crc32c_small_kernel(const uint8_t*, SmallList, uint32_t*, uint32_t,
-                                    const DevTables*);
+                                    const DevTables*, uint8_t*);
 }  // namespace dev
 }  // namespace wipdb
 
@@ -209,7 +209,7 @@ int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
     const int pgrid = static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8));
     hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st,
                        static_cast<const uint8_t*>(base), off, len, init,
-                       static_cast<uint64_t>(n), sl);
+                       static_cast<uint64_t>(n), sl, 0u);
     rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
   }
   // the spans kernel first: it leaves the partial CRCs of the spans it cuts
@@ -220,7 +220,8 @@ int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
   if (rc == HCRC_OK) {
     hipLaunchKernelGGL(wipdb::dev::crc32c_small_kernel, dim3(ctx->num_cu),
                        dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
-                       static_cast<const uint8_t*>(base), sl, out, mask, ctx->d_tab);
+                       static_cast<const uint8_t*>(base), sl, out, mask, ctx->d_tab,
+                       nullptr);
     rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
   }
   if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
@@ -653,10 +654,63 @@ int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
   return HCRC_OK;
 }
 
-int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
-                      const uint32_t* d_lengths, uint8_t* d_status, size_t count,
-                      void* stream) {
+namespace {
+// One verify launch (count < 2^31); with split, blocks of at most kSmallMax
+// bytes and the remainders of blocks that just overrun a segment go to the
+// small kernel, the cut blocks' partial CRCs passing through `partial`.
+int LaunchVerify(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
+                 uint8_t* status, size_t n, bool split, hipStream_t st) {
+  uint8_t* scratch = nullptr;
+  wipdb::dev::SmallList sl{};
+  uint32_t* partial = nullptr;
+  uint32_t kflags = 0;
+  int rc = HCRC_OK;
+  if (split) {
+    HCRC_CHECK(hipMallocAsync(reinterpret_cast<void**>(&scratch), n * 24 + 64, st));
+    sl.off = reinterpret_cast<uint64_t*>(scratch);
+    sl.len = reinterpret_cast<uint32_t*>(scratch + n * 8);
+    sl.init = sl.len + n;
+    sl.id = sl.init + n;
+    partial = sl.id + n;
+    sl.count = partial + n;
+    kflags = wipdb::dev::kFlagSkipSmall | wipdb::dev::kFlagSplitRem;
+    if (hipMemsetAsync(sl.count, 0, 4, st) != hipSuccess) rc = HCRC_ERR_HIP;
+    if (rc == HCRC_OK) {
+      const int pgrid =
+          static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8));
+      hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st,
+                         base, off, len, nullptr, static_cast<uint64_t>(n), sl, 1u);
+      rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+    }
+  }
+  if (rc == HCRC_OK) {
+    WorkPool wp;
+    rc = wp.Acquire(ctx, st);
+    if (rc == HCRC_OK) {
+      hipLaunchKernelGGL(wipdb::dev::crc32c_verify_kernel, dim3(LaunchGrid(ctx, n)),
+                         dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st, base, off, len,
+                         status, static_cast<uint64_t>(n), ctx->d_tab, wp.p, kflags, partial);
+      rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+      const int rr = wp.Release(st);
+      if (rc == HCRC_OK) rc = rr;
+    }
+  }
+  if (split && rc == HCRC_OK) {
+    hipLaunchKernelGGL(wipdb::dev::crc32c_small_kernel, dim3(ctx->num_cu),
+                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st, base, sl, partial,
+                       wipdb::dev::kFlagVerify, ctx->d_tab, status);
+    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+  }
+  if (scratch && hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
+  return rc;
+}
+}  // namespace
+
+int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
+                         const uint32_t* d_lengths, uint8_t* d_status, size_t count, int flags,
+                         void* stream) {
   if (!ctx) return HCRC_ERR_INVALID;
+  if (flags & ~HCRC_SPLIT_SMALL) return HCRC_ERR_INVALID;
   if (count && (!d_base || !d_offsets || !d_lengths || !d_status))
     return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
@@ -665,19 +719,18 @@ int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offse
   const hipStream_t st = StreamOf(ctx, stream);
   for (size_t pos = 0; pos < count; pos += kMaxLaunchSpans) {
     const size_t n = std::min(count - pos, kMaxLaunchSpans);
-    WorkPool wp;
-    int rc = wp.Acquire(ctx, st);
-    if (rc != HCRC_OK) return rc;
-    hipLaunchKernelGGL(wipdb::dev::crc32c_verify_kernel, dim3(LaunchGrid(ctx, n)),
-                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
-                       static_cast<const uint8_t*>(d_base), d_offsets + pos, d_lengths + pos,
-                       d_status + pos, static_cast<uint64_t>(n), ctx->d_tab, wp.p);
-    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
-    const int rr = wp.Release(st);
-    if (rc == HCRC_OK) rc = rr;
+    const int rc = LaunchVerify(ctx, static_cast<const uint8_t*>(d_base), d_offsets + pos,
+                                d_lengths + pos, d_status + pos, n,
+                                (flags & HCRC_SPLIT_SMALL) != 0, st);
     if (rc != HCRC_OK) return rc;
   }
   return HCRC_OK;
+}
+
+int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
+                      const uint32_t* d_lengths, uint8_t* d_status, size_t count,
+                      void* stream) {
+  return hcrc_verify_async_ex(ctx, d_base, d_offsets, d_lengths, d_status, count, 0, stream);
 }
 
 int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
