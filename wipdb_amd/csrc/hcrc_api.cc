@@ -87,6 +87,9 @@ struct PoolBuf {
 
 struct hcrc_ctx {
   std::vector<PoolBuf> pools;  // under mu
+  // stream-ordered scratch (small-span lists) comes from a private pool that
+  // keeps its memory mapped between calls (release threshold: never)
+  hipMemPool_t scratch_pool = nullptr;
   int device = -1;
   hipStream_t stream = nullptr;
   DevTables* d_tab = nullptr;
@@ -162,6 +165,12 @@ struct WorkPool {
   }
 };
 
+// partition kernel workgroups per CU: enough waves to hide the descriptor
+// loads' latency (2 per CU: 187 us for 1 M spans, 16: ~50 us)
+#ifndef WIPDB_PART_WG
+#define WIPDB_PART_WG 16
+#endif
+
 // The kernels keep span indices in 32 bits: larger batches go in pieces.
 constexpr size_t kMaxLaunchSpans = size_t(1) << 31;
 
@@ -189,14 +198,15 @@ int LaunchSpansKernel(hcrc_ctx* ctx, const void* base, const uint64_t* off,
 // HCRC_SPLIT_SMALL: the spans of at most kSmallMax bytes are compacted by
 // the partition kernel and checksummed 8 per wave slot by the small kernel;
 // the spans kernel skips them.  Everything is ordered on `st`, the scratch
-// is stream-ordered (hipMallocAsync / hipFreeAsync), so concurrent calls on
+// is stream-ordered (hipMallocFromPoolAsync / hipFreeAsync), so concurrent calls on
 // different streams never share it.
 int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
                 const uint32_t* init, uint32_t* out, size_t count, uint32_t mask,
                 hipStream_t st) {
   const size_t n = count;
   uint8_t* scratch = nullptr;
-  HCRC_CHECK(hipMallocAsync(reinterpret_cast<void**>(&scratch), n * 20 + 64, st));
+  HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), n * 20 + 64,
+                                    ctx->scratch_pool, st));
   wipdb::dev::SmallList sl;
   sl.off = reinterpret_cast<uint64_t*>(scratch);
   sl.len = reinterpret_cast<uint32_t*>(scratch + n * 8);
@@ -206,7 +216,7 @@ int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
   int rc = HCRC_OK;
   if (hipMemsetAsync(sl.count, 0, 4, st) != hipSuccess) rc = HCRC_ERR_HIP;
   if (rc == HCRC_OK) {
-    const int pgrid = static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8));
+    const int pgrid = static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * WIPDB_PART_WG));
     hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st,
                        static_cast<const uint8_t*>(base), off, len, init,
                        static_cast<uint64_t>(n), sl, 0u);
@@ -526,6 +536,15 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
   HCRC_CHECK(hipGetDeviceProperties(&prop, device));
   ctx->num_cu = prop.multiProcessorCount;
   HCRC_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  {
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
+    HCRC_CHECK(hipMemPoolCreate(&ctx->scratch_pool, &props));
+    uint64_t keep = ~uint64_t(0);
+    HCRC_CHECK(hipMemPoolSetAttribute(ctx->scratch_pool, hipMemPoolAttrReleaseThreshold, &keep));
+  }
   const unsigned lds = wipdb::dev::kLdsBytes;
   HCRC_CHECK(hipFuncSetAttribute(
       reinterpret_cast<const void*>(wipdb::dev::crc32c_spans_kernel),
@@ -583,6 +602,10 @@ int hcrc_ctx_destroy(hcrc_ctx* ctx) {
   }
   if (ctx->d_tab) (void)hipFree(ctx->d_tab);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->scratch_pool) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemPoolDestroy(ctx->scratch_pool);
+  }
   delete ctx;
   return HCRC_OK;
 }
@@ -666,7 +689,8 @@ int LaunchVerify(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
   uint32_t kflags = 0;
   int rc = HCRC_OK;
   if (split) {
-    HCRC_CHECK(hipMallocAsync(reinterpret_cast<void**>(&scratch), n * 24 + 64, st));
+    HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), n * 24 + 64,
+                                      ctx->scratch_pool, st));
     sl.off = reinterpret_cast<uint64_t*>(scratch);
     sl.len = reinterpret_cast<uint32_t*>(scratch + n * 8);
     sl.init = sl.len + n;
@@ -677,7 +701,7 @@ int LaunchVerify(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
     if (hipMemsetAsync(sl.count, 0, 4, st) != hipSuccess) rc = HCRC_ERR_HIP;
     if (rc == HCRC_OK) {
       const int pgrid =
-          static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8));
+          static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * WIPDB_PART_WG));
       hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st,
                          base, off, len, nullptr, static_cast<uint64_t>(n), sl, 1u);
       rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
