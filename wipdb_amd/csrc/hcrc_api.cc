@@ -43,7 +43,10 @@ __global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*,
                                   uint64_t);
 __global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
 __global__ void crc32c_partition_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
-                                        const uint32_t*, uint64_t, SmallList, uint32_t);
+                                        const uint32_t*, uint64_t, SmallList, uint32_t,
+                                        SmallList);
+// instantiated for 8-lane (257..1024 B) and 2-lane (<= 256 B) subgroups
+template <int SGT>
 __global__ void crc32c_small_kernel(const uint8_t*, SmallList, uint32_t*, uint32_t,
                                     const DevTables*, uint8_t*);
 }  // namespace dev
@@ -195,6 +198,39 @@ int LaunchSpansKernel(hcrc_ctx* ctx, const void* base, const uint64_t* off,
   return HCRC_OK;
 }
 
+// Two small-span lists (8-lane and 2-lane subgroups) carved out of one
+// scratch block of n * 40 + 64 bytes; returns their two counters.
+uint32_t* CarveSmallLists(uint8_t* scratch, size_t n, wipdb::dev::SmallList* sl,
+                          wipdb::dev::SmallList* tl) {
+  wipdb::dev::SmallList* l[2] = {sl, tl};
+  uint8_t* p = scratch;
+  for (auto* x : l) {
+    x->off = reinterpret_cast<uint64_t*>(p);
+    x->len = reinterpret_cast<uint32_t*>(p + n * 8);
+    x->init = x->len + n;
+    x->id = x->init + n;
+    p += n * 20;
+  }
+  uint32_t* counts = reinterpret_cast<uint32_t*>(p);
+  sl->count = counts;
+  tl->count = counts + 1;
+  return counts;
+}
+
+// The small-span kernel over both lists (each launch exits at once when its
+// list is empty).
+int LaunchSmall(hcrc_ctx* ctx, const uint8_t* base, const wipdb::dev::SmallList& sl,
+                const wipdb::dev::SmallList& tl, uint32_t* out, uint32_t flags, uint8_t* status,
+                hipStream_t st) {
+  hipLaunchKernelGGL((wipdb::dev::crc32c_small_kernel<8>), dim3(ctx->num_cu),
+                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st, base, sl, out, flags,
+                     ctx->d_tab, status);
+  hipLaunchKernelGGL((wipdb::dev::crc32c_small_kernel<2>), dim3(ctx->num_cu),
+                     dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st, base, tl, out, flags,
+                     ctx->d_tab, status);
+  return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
+}
+
 // HCRC_SPLIT_SMALL: the spans of at most kSmallMax bytes are compacted by
 // the partition kernel and checksummed 8 per wave slot by the small kernel;
 // the spans kernel skips them.  Everything is ordered on `st`, the scratch
@@ -205,21 +241,17 @@ int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                 hipStream_t st) {
   const size_t n = count;
   uint8_t* scratch = nullptr;
-  HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), n * 20 + 64,
+  HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), n * 40 + 64,
                                     ctx->scratch_pool, st));
-  wipdb::dev::SmallList sl;
-  sl.off = reinterpret_cast<uint64_t*>(scratch);
-  sl.len = reinterpret_cast<uint32_t*>(scratch + n * 8);
-  sl.init = sl.len + n;
-  sl.id = sl.init + n;
-  sl.count = sl.id + n;
+  wipdb::dev::SmallList sl, tl;
+  uint32_t* counts = CarveSmallLists(scratch, n, &sl, &tl);
   int rc = HCRC_OK;
-  if (hipMemsetAsync(sl.count, 0, 4, st) != hipSuccess) rc = HCRC_ERR_HIP;
+  if (hipMemsetAsync(counts, 0, 8, st) != hipSuccess) rc = HCRC_ERR_HIP;
   if (rc == HCRC_OK) {
     const int pgrid = static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * WIPDB_PART_WG));
     hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st,
                        static_cast<const uint8_t*>(base), off, len, init,
-                       static_cast<uint64_t>(n), sl, 0u);
+                       static_cast<uint64_t>(n), sl, 0u, tl);
     rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
   }
   // the spans kernel first: it leaves the partial CRCs of the spans it cuts
@@ -227,13 +259,8 @@ int LaunchSplit(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
   if (rc == HCRC_OK)
     rc = LaunchSpansKernel(ctx, base, off, len, init, out, count,
                            mask | wipdb::dev::kFlagSkipSmall | wipdb::dev::kFlagSplitRem, st);
-  if (rc == HCRC_OK) {
-    hipLaunchKernelGGL(wipdb::dev::crc32c_small_kernel, dim3(ctx->num_cu),
-                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
-                       static_cast<const uint8_t*>(base), sl, out, mask, ctx->d_tab,
-                       nullptr);
-    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
-  }
+  if (rc == HCRC_OK)
+    rc = LaunchSmall(ctx, static_cast<const uint8_t*>(base), sl, tl, out, mask, nullptr, st);
   if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
   return rc;
 }
@@ -556,7 +583,10 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
       reinterpret_cast<const void*>(wipdb::dev::crc32c_verify_kernel),
       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   HCRC_CHECK(hipFuncSetAttribute(
-      reinterpret_cast<const void*>(wipdb::dev::crc32c_small_kernel),
+      reinterpret_cast<const void*>(wipdb::dev::crc32c_small_kernel<8>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::dev::crc32c_small_kernel<2>),
       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   HCRC_CHECK(hipFuncSetAttribute(
       reinterpret_cast<const void*>(wipdb::dev::readstream_kernel),
@@ -684,26 +714,22 @@ namespace {
 int LaunchVerify(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
                  uint8_t* status, size_t n, bool split, hipStream_t st) {
   uint8_t* scratch = nullptr;
-  wipdb::dev::SmallList sl{};
+  wipdb::dev::SmallList sl{}, tl{};
   uint32_t* partial = nullptr;
   uint32_t kflags = 0;
   int rc = HCRC_OK;
   if (split) {
-    HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), n * 24 + 64,
+    HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), n * 44 + 64,
                                       ctx->scratch_pool, st));
-    sl.off = reinterpret_cast<uint64_t*>(scratch);
-    sl.len = reinterpret_cast<uint32_t*>(scratch + n * 8);
-    sl.init = sl.len + n;
-    sl.id = sl.init + n;
-    partial = sl.id + n;
-    sl.count = partial + n;
+    partial = reinterpret_cast<uint32_t*>(scratch);
+    uint32_t* counts = CarveSmallLists(scratch + n * 4, n, &sl, &tl);
     kflags = wipdb::dev::kFlagSkipSmall | wipdb::dev::kFlagSplitRem;
-    if (hipMemsetAsync(sl.count, 0, 4, st) != hipSuccess) rc = HCRC_ERR_HIP;
+    if (hipMemsetAsync(counts, 0, 8, st) != hipSuccess) rc = HCRC_ERR_HIP;
     if (rc == HCRC_OK) {
       const int pgrid =
           static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * WIPDB_PART_WG));
       hipLaunchKernelGGL(wipdb::dev::crc32c_partition_kernel, dim3(pgrid), dim3(256), 0, st,
-                         base, off, len, nullptr, static_cast<uint64_t>(n), sl, 1u);
+                         base, off, len, nullptr, static_cast<uint64_t>(n), sl, 1u, tl);
       rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
     }
   }
@@ -719,12 +745,8 @@ int LaunchVerify(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
       if (rc == HCRC_OK) rc = rr;
     }
   }
-  if (split && rc == HCRC_OK) {
-    hipLaunchKernelGGL(wipdb::dev::crc32c_small_kernel, dim3(ctx->num_cu),
-                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st, base, sl, partial,
-                       wipdb::dev::kFlagVerify, ctx->d_tab, status);
-    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
-  }
+  if (split && rc == HCRC_OK)
+    rc = LaunchSmall(ctx, base, sl, tl, partial, wipdb::dev::kFlagVerify, status, st);
   if (scratch && hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
   return rc;
 }
