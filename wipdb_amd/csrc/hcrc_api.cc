@@ -280,7 +280,10 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off,
 // Host pieces: split when enough spans are small, or just over a segment
 // (a table block of 4 KiB + its last entry: the remainder goes to the small
 // kernel), for the small kernel to pay for its two extra launches.
-constexpr size_t kAutoSplitMin = 256;
+#ifndef WIPDB_AUTO_SPLIT_MIN
+#define WIPDB_AUTO_SPLIT_MIN 256
+#endif
+constexpr size_t kAutoSplitMin = WIPDB_AUTO_SPLIT_MIN;
 
 int AutoSplit(const uint32_t* lengths, size_t n) {
   size_t small = 0;
