@@ -15,9 +15,12 @@ run() {  # name timeout cmd...
   echo "=== $name rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.log" | tail -2
   if [ $rc -ne 0 ]; then echo "ABORT after $name"; exit $rc; fi
 }
-run ${P}_bench 300 python bench.py --steps 20 --warmup 3 --cpu-seconds 10 --readstream
-run ${P}_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline
+run ${P}_bench 300 python bench.py --steps 50 --warmup 30 --cpu-seconds 10 --readstream
+run ${P}_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 50 --warmup 30 --no-cpu-baseline
 run ${P}_pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${P}_pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
 run ${P}_pmc_write 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${P}_pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
-run ${P}_cfg4_shard 300 python bench.py --blocks 8388608 --steps 5 --warmup 1 --no-cpu-baseline
+# the stats average every dispatch (the warmup's clock-settling launches
+# too); this is the average of the 50 timed ones, as bench.py reports
+run ${P}_prof_timed 60 python scripts/trace_tail.py gpurun_out/${P}_prof crc32c_spans_kernel 50
+run ${P}_cfg4_shard 300 python bench.py --blocks 8388608 --steps 10 --warmup 5 --no-cpu-baseline
 echo ALLDONE

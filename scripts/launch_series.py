@@ -1,0 +1,56 @@
+"""Per-launch kernel time of the headline batch (1 M x 4 KiB, spans entry
+point) over a long back-to-back series: does the rate settle after the
+first launches (clocks, TLB), and how much do launches vary?
+
+  python scripts/launch_series.py [--launches 200] [--blocks N] [--idle-ms 0]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from wipdb_amd.crc32c import Engine  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--launches", type=int, default=200)
+    p.add_argument("--blocks", type=int, default=1 << 20)
+    p.add_argument("--idle-ms", type=float, default=0.0, help="host sleep between launches")
+    a = p.parse_args()
+    dev = torch.device("cuda", 0)
+    eng = Engine(0)
+    n = a.blocks
+    data = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev)
+    eng.fill_splitmix64_device(data, 0x4B10C5, stream=st.cuda_stream)
+    offs = torch.arange(n, dtype=torch.int64, device=dev) * 4096
+    lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.launches)]
+    for s, e in ev:
+        s.record(st)
+        eng.batch_device(data, offs, lens, None, out, stream=st.cuda_stream)
+        e.record(st)
+        if a.idle_ms:
+            torch.cuda.synchronize(dev)
+            time.sleep(a.idle_ms / 1e3)
+    torch.cuda.synchronize(dev)
+    ms = np.array([s.elapsed_time(e) for s, e in ev])
+    res = {"blocks": n, "idle_ms": a.idle_ms, "first10": [round(float(x), 4) for x in ms[:10]]}
+    for lo, hi in [(0, 3), (3, 23), (3, 53), (20, 70), (50, 100), (100, 200)]:
+        if hi <= len(ms):
+            res[f"mean[{lo}:{hi}]"] = round(float(ms[lo:hi].mean()), 4)
+    res["pct(5,50,95)"] = [round(float(x), 4) for x in np.percentile(ms, [5, 50, 95])]
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
