@@ -9,7 +9,7 @@ tail -1 gpurun_out/gt.log
 for r in 1 2; do for v in $VARIANTS; do
   if [ $v = default ]; then unset WIPDB_HCRC_LIB; else export WIPDB_HCRC_LIB=$PWD/build/variants/$v/libhip_crc32c_batch.so; fi
   for L in $LENS; do
-    timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --len $L > gpurun_out/bl.log 2>&1 || { tail -5 gpurun_out/bl.log; exit 1; }
+    timeout -k 10 200 python bench.py --steps 50 --warmup 30 --no-cpu-baseline --len $L > gpurun_out/bl.log 2>&1 || { tail -5 gpurun_out/bl.log; exit 1; }
     echo "$v len $L $(grep -o "\"kernel_avg_ms\": [0-9.]*" gpurun_out/bl.log)"
   done
   case ",$EXTRA," in *,verify,*)
