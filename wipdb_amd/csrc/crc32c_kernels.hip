@@ -56,6 +56,7 @@
 //   WIPDB_ILP      chains interleaved per feed step
 //   WIPDB_LOADONLY diagnostic: the loads and ring without the CRC work
 //   WIPDB_NOFOLD   diagnostic: the scan without the cross-chain fold
+//   WIPDB_NO_STORE diagnostic: the spans kernel's result stores compiled out
 //   WIPDB_NO_TABLES, WIPDB_RS_UNROLL, WIPDB_RS_SPLIT: diagnostics for the
 //                  load-only skeleton and the read-stream kernel
 //                  (scripts/stream_probe.py)
@@ -137,6 +138,9 @@
 // g_timeline; hcrc_debug_timeline copies it out (scripts/timeline_probe.py)
 #ifndef WIPDB_TIMELINE
 #define WIPDB_TIMELINE 0
+#endif
+#ifndef WIPDB_NO_STORE
+#define WIPDB_NO_STORE 0
 #endif
 
 
@@ -1430,7 +1434,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_spans_kernel(
   run_waves(src, wave_id(), grid_waves(), tab, flags & (kFlagSkipSmall | kFlagSplitRem), work,
             [&](uint64_t span, uint32_t crc, int g, uint32_t, bool partial) {
     // a partial CRC (remainder left to the small kernel) stays unmasked
+#if WIPDB_NO_STORE  // diagnostic: what the scattered 4-byte result stores cost (wrong results)
+    if (group_leader(g) && crc == 0x9E3779B9u) out[span] = crc;
+#else
     if (group_leader(g)) out[span] = msk && !partial ? mask_crc(crc) : crc;
+#endif
   });
 #if WIPDB_TIMELINE
   if (stamp) tl[2 + (threadIdx.x >> 6)] = wall_clock64();
