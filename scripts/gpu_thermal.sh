@@ -1,0 +1,18 @@
+# Does the headline kernel slow down as the card warms?  Long launch series
+# back to back, with the card's temperature / clocks / power sampled by
+# rocm-smi while each series runs.
+set -o pipefail
+mkdir -p gpurun_out
+for i in 1 2 3 4; do
+  timeout -k 10 120 python scripts/launch_series.py --launches ${LAUNCHES:-6000} > gpurun_out/th_$i.log 2>&1 &
+  pid=$!
+  : > gpurun_out/th_smi_$i.log
+  for t in ${SAMPLES:-3 1 1 1 1}; do
+    sleep $t
+    (rocm-smi --showclocks --showpower 2>&1 || true) | grep -iE "sclk|Package Power" | grep -o '([0-9]*Mhz)\|: [0-9.]*$' | tr -d ' :()\n' >> gpurun_out/th_smi_$i.log
+    echo -n " | " >> gpurun_out/th_smi_$i.log
+  done
+  wait $pid || { tail -5 gpurun_out/th_$i.log; exit 1; }
+  echo "series $i: $(grep -v amdgpu.ids gpurun_out/th_$i.log | grep -o '"per500": \[[0-9., ]*\]' | tr '\n' ' ')"
+  echo "  smi: $(cat gpurun_out/th_smi_$i.log)"
+done

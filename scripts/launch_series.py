@@ -48,6 +48,8 @@ def main():
     for lo, hi in [(0, 3), (3, 23), (3, 53), (20, 70), (50, 100), (100, 200)]:
         if hi <= len(ms):
             res[f"mean[{lo}:{hi}]"] = round(float(ms[lo:hi].mean()), 4)
+    if len(ms) >= 1000:
+        res["per500"] = [round(float(ms[i:i + 500].mean()), 4) for i in range(0, len(ms) - 499, 500)]
     res["pct(5,50,95)"] = [round(float(x), 4) for x in np.percentile(ms, [5, 50, 95])]
     print(json.dumps(res), flush=True)
 
