@@ -22,6 +22,8 @@ def main():
     p.add_argument("--launches", type=int, default=200)
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--idle-ms", type=float, default=0.0, help="host sleep between launches")
+    p.add_argument("--what", choices=["spans", "readstream"], default="spans",
+                   help="readstream: the same blocks through readstream_kernel (no CRC work)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     eng = Engine(0)
@@ -37,14 +39,17 @@ def main():
           for _ in range(a.launches)]
     for s, e in ev:
         s.record(st)
-        eng.batch_device(data, offs, lens, None, out, stream=st.cuda_stream)
+        if a.what == "spans":
+            eng.batch_device(data, offs, lens, None, out, stream=st.cuda_stream)
+        else:
+            eng.readstream_device(data, 4096, 4096, n, out, stream=st.cuda_stream)
         e.record(st)
         if a.idle_ms:
             torch.cuda.synchronize(dev)
             time.sleep(a.idle_ms / 1e3)
     torch.cuda.synchronize(dev)
     ms = np.array([s.elapsed_time(e) for s, e in ev])
-    res = {"blocks": n, "idle_ms": a.idle_ms, "first10": [round(float(x), 4) for x in ms[:10]]}
+    res = {"what": a.what, "blocks": n, "idle_ms": a.idle_ms, "first10": [round(float(x), 4) for x in ms[:10]]}
     for lo, hi in [(0, 3), (3, 23), (3, 53), (20, 70), (50, 100), (100, 200)]:
         if hi <= len(ms):
             res[f"mean[{lo}:{hi}]"] = round(float(ms[lo:hi].mean()), 4)

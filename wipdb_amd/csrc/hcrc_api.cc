@@ -131,9 +131,15 @@ void BuildDevTables(DevTables* dt) {
   memcpy(dt->head0, T.head0, sizeof(dt->head0));
 }
 
+// WIPDB_GRID_CAP (diagnostic build knob): at most this many workgroups, i.e.
+// CUs, for the spans kernels (the package-power experiments)
+#ifndef WIPDB_GRID_CAP
+#define WIPDB_GRID_CAP 0
+#endif
 int LaunchGrid(hcrc_ctx* ctx, size_t count) {
   size_t need = (count + wipdb::dev::kSpansPerWG - 1) / wipdb::dev::kSpansPerWG;
   size_t g = std::min<size_t>(need, size_t(ctx->num_cu));
+  if (WIPDB_GRID_CAP > 0) g = std::min<size_t>(g, size_t(WIPDB_GRID_CAP));
   return static_cast<int>(std::max<size_t>(g, 1));
 }
 
