@@ -22,22 +22,32 @@ def main():
     p.add_argument("--launches", type=int, default=200)
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--idle-ms", type=float, default=0.0, help="host sleep between launches")
+    p.add_argument("--buffers", type=int, default=1,
+                   help="allocate this many copies of the batch and run them round robin "
+                        "(is the rate a property of the allocation?)")
+    p.add_argument("--pre-alloc-gib", type=float, default=0.0,
+                   help="allocate (and keep) this much device memory before the batches")
     p.add_argument("--what", choices=["spans", "readstream"], default="spans",
                    help="readstream: the same blocks through readstream_kernel (no CRC work)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     eng = Engine(0)
     n = a.blocks
-    data = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream(dev)
-    eng.fill_splitmix64_device(data, 0x4B10C5, stream=st.cuda_stream)
+    pre = (torch.empty(int(a.pre_alloc_gib * 2**30), dtype=torch.uint8, device=dev)
+           if a.pre_alloc_gib else None)
+    bufs = []
+    for _ in range(a.buffers):
+        bufs.append(torch.empty(n * 4096, dtype=torch.uint8, device=dev))
+        eng.fill_splitmix64_device(bufs[-1], 0x4B10C5, stream=st.cuda_stream)
     offs = torch.arange(n, dtype=torch.int64, device=dev) * 4096
     lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.launches)]
-    for s, e in ev:
+    for i, (s, e) in enumerate(ev):
+        data = bufs[i % a.buffers]
         s.record(st)
         if a.what == "spans":
             eng.batch_device(data, offs, lens, None, out, stream=st.cuda_stream)
@@ -55,6 +65,9 @@ def main():
             res[f"mean[{lo}:{hi}]"] = round(float(ms[lo:hi].mean()), 4)
     if len(ms) >= 1000:
         res["per500"] = [round(float(ms[i:i + 500].mean()), 4) for i in range(0, len(ms) - 499, 500)]
+    if a.buffers > 1:
+        res["per_buffer"] = [round(float(ms[b::a.buffers][10:].mean()), 4) for b in range(a.buffers)]
+        res["buffer_addr_MiB"] = [b.data_ptr() >> 20 for b in bufs]
     res["pct(5,50,95)"] = [round(float(x), 4) for x in np.percentile(ms, [5, 50, 95])]
     print(json.dumps(res), flush=True)
 
