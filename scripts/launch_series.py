@@ -27,7 +27,9 @@ def main():
                         "(is the rate a property of the allocation?)")
     p.add_argument("--pre-alloc-gib", type=float, default=0.0,
                    help="allocate (and keep) this much device memory before the batches")
-    p.add_argument("--what", choices=["spans", "readstream"], default="spans",
+    p.add_argument("--desc-first", action="store_true",
+                   help="allocate the descriptor and output columns before the batches")
+    p.add_argument("--what", choices=["spans", "strided", "readstream"], default="spans",
                    help="readstream: the same blocks through readstream_kernel (no CRC work)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
@@ -36,13 +38,18 @@ def main():
     st = torch.cuda.current_stream(dev)
     pre = (torch.empty(int(a.pre_alloc_gib * 2**30), dtype=torch.uint8, device=dev)
            if a.pre_alloc_gib else None)
+    if a.desc_first:
+        offs = torch.arange(n, dtype=torch.int64, device=dev) * 4096
+        lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
     bufs = []
     for _ in range(a.buffers):
         bufs.append(torch.empty(n * 4096, dtype=torch.uint8, device=dev))
         eng.fill_splitmix64_device(bufs[-1], 0x4B10C5, stream=st.cuda_stream)
-    offs = torch.arange(n, dtype=torch.int64, device=dev) * 4096
-    lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
-    out = torch.empty(n, dtype=torch.int32, device=dev)
+    if not a.desc_first:
+        offs = torch.arange(n, dtype=torch.int64, device=dev) * 4096
+        lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.launches)]
@@ -51,6 +58,8 @@ def main():
         s.record(st)
         if a.what == "spans":
             eng.batch_device(data, offs, lens, None, out, stream=st.cuda_stream)
+        elif a.what == "strided":
+            eng.batch_strided_device(data, 4096, 4096, n, 0, out, stream=st.cuda_stream)
         else:
             eng.readstream_device(data, 4096, 4096, n, out, stream=st.cuda_stream)
         e.record(st)
