@@ -17,6 +17,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from wipdb_amd.crc32c import Engine  # noqa: E402
 
 
+def span_order(order, n, dev):
+    idx = torch.arange(n, dtype=torch.int64, device=dev)
+    if order == "natural":
+        return idx
+    if order == "random":
+        g = torch.Generator(device="cpu").manual_seed(7)
+        return torch.randperm(n, generator=g).to(dev)
+    G = torch.cuda.get_device_properties(dev).multi_processor_count * 16 * 2
+    assert n % G == 0
+    q, k = idx % G, idx // G
+    if order == "group":
+        return q * (n // G) + k
+    per_wg = 32
+    return (q // per_wg) * (n // (G // per_wg)) + k * per_wg + q % per_wg
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--launches", type=int, default=200)
@@ -29,6 +45,9 @@ def main():
                    help="allocate (and keep) this much device memory before the batches")
     p.add_argument("--desc-first", action="store_true",
                    help="allocate the descriptor and output columns before the batches")
+    p.add_argument("--order", choices=["natural", "group", "cu", "random"], default="natural",
+                   help="span order of the descriptor columns (bench.py --order; random: a "
+                        "seeded permutation)")
     p.add_argument("--what", choices=["spans", "strided", "readstream"], default="spans",
                    help="readstream: the same blocks through readstream_kernel (no CRC work)")
     a = p.parse_args()
@@ -39,7 +58,7 @@ def main():
     pre = (torch.empty(int(a.pre_alloc_gib * 2**30), dtype=torch.uint8, device=dev)
            if a.pre_alloc_gib else None)
     if a.desc_first:
-        offs = torch.arange(n, dtype=torch.int64, device=dev) * 4096
+        offs = span_order(a.order, n, dev) * 4096
         lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
     bufs = []
@@ -47,7 +66,7 @@ def main():
         bufs.append(torch.empty(n * 4096, dtype=torch.uint8, device=dev))
         eng.fill_splitmix64_device(bufs[-1], 0x4B10C5, stream=st.cuda_stream)
     if not a.desc_first:
-        offs = torch.arange(n, dtype=torch.int64, device=dev) * 4096
+        offs = span_order(a.order, n, dev) * 4096
         lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
