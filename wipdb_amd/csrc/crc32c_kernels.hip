@@ -139,6 +139,11 @@
 #ifndef WIPDB_TIMELINE
 #define WIPDB_TIMELINE 0
 #endif
+// WIPDB_TAIL_SELF: slots without a ragged tail load their own first chunk
+// as the tail chunk instead of a device-wide dummy line
+#ifndef WIPDB_TAIL_SELF
+#define WIPDB_TAIL_SELF 0
+#endif
 #ifndef WIPDB_NO_STORE
 #define WIPDB_NO_STORE 0
 #endif
@@ -860,9 +865,17 @@ __device__ __forceinline__ void issue_seg(const Slot (&s)[S], uint32_t lane, con
 #pragma unroll
   for (int g = 0; g < S; ++g) {
     const uint32_t hn = static_cast<uint32_t>(s[g].start & 15u) + s[g].n();
+#if WIPDB_TAIL_SELF
+    // no ragged tail: read the segment's own first chunk (a line the slot
+    // loads anyway) instead of one device-wide dummy line
+    tail_g[g] = (s[g].flags() & kSlotValid)
+                    ? (s[g].start & ~uint64_t(15)) + ((hn & 15u) ? (hn & ~15u) : 0u)
+                    : reinterpret_cast<uint64_t>(dummy);
+#else
     tail_g[g] = ((s[g].flags() & kSlotValid) && (hn & 15u))
                     ? (s[g].start & ~uint64_t(15)) + (hn & ~15u)
                     : reinterpret_cast<uint64_t>(dummy);
+#endif
   }
   d[NL] = *reinterpret_cast<g_u32x4*>(gsel(lane >= static_cast<uint32_t>(G), tail_g[0], tail_g[1]));
   uint32_t pad_g[S];
