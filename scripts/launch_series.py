@@ -50,6 +50,10 @@ def main():
                         "seeded permutation)")
     p.add_argument("--what", choices=["spans", "strided", "readstream"], default="spans",
                    help="readstream: the same blocks through readstream_kernel (no CRC work)")
+    p.add_argument("--pre-what", choices=["spans", "strided", "readstream"], default=None,
+                   help="run this many untimed launches of another kernel first (--pre-launches)")
+    p.add_argument("--pre-launches", type=int, default=0)
+    p.add_argument("--series", action="store_true", help="print every launch time")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     eng = Engine(0)
@@ -70,17 +74,23 @@ def main():
         lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
+
+    def launch(what, data):
+        if what == "spans":
+            eng.batch_device(data, offs, lens, None, out, stream=st.cuda_stream)
+        elif what == "strided":
+            eng.batch_strided_device(data, 4096, 4096, n, 0, out, stream=st.cuda_stream)
+        else:
+            eng.readstream_device(data, 4096, 4096, n, out, stream=st.cuda_stream)
+
+    for i in range(a.pre_launches):
+        launch(a.pre_what, bufs[i % a.buffers])
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.launches)]
     for i, (s, e) in enumerate(ev):
         data = bufs[i % a.buffers]
         s.record(st)
-        if a.what == "spans":
-            eng.batch_device(data, offs, lens, None, out, stream=st.cuda_stream)
-        elif a.what == "strided":
-            eng.batch_strided_device(data, 4096, 4096, n, 0, out, stream=st.cuda_stream)
-        else:
-            eng.readstream_device(data, 4096, 4096, n, out, stream=st.cuda_stream)
+        launch(a.what, data)
         e.record(st)
         if a.idle_ms:
             torch.cuda.synchronize(dev)
@@ -96,6 +106,8 @@ def main():
     if a.buffers > 1:
         res["per_buffer"] = [round(float(ms[b::a.buffers][10:].mean()), 4) for b in range(a.buffers)]
         res["buffer_addr_MiB"] = [b.data_ptr() >> 20 for b in bufs]
+    if a.series:
+        res["series"] = [round(float(x), 3) for x in ms]
     res["pct(5,50,95)"] = [round(float(x), 4) for x in np.percentile(ms, [5, 50, 95])]
     print(json.dumps(res), flush=True)
 

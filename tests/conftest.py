@@ -125,6 +125,10 @@ def kats() -> dict:
 
 @pytest.fixture(scope="session")
 def golden_spans():
+    return load_golden_spans()
+
+
+def load_golden_spans() -> dict:
     from tests.golden.common import splitmix64_bytes
     with open(os.path.join(GOLDEN, "spans.json")) as f:
         d = json.load(f)

@@ -1,0 +1,105 @@
+// crc32c_lds.h -- LDS layout of the LDS-staged CRC32C kernels
+// (crc32c_lds.hip) and the host builder of the table image they load.
+// Shared by the device code and hcrc_api.cc.  DESIGN.md section 3.
+//
+// One 1024-thread workgroup (16 waves) per CU owns all 160 KiB of LDS:
+//
+//   [0, 32 KiB)     fold level-2 tables, 256 rows of 128 B: row b holds
+//                   entry (c, p) at (4c + p) * 4 = shift(b << 8p, 512c bytes)
+//                   for c = 1..7; the c = 0 column (bytes 0..15 of each row,
+//                   an identity shift nobody looks up) holds the misc words.
+//   [32, 96 KiB)    main region, 256 rows of 256 B:
+//                   bytes [0, 128): slicing-by-4 tables, slot t (0..3) x
+//                   replica r (0..7) at 32t + 4r = T[3 - t][b] (the table of
+//                   byte position t of a word);
+//                   bytes [128, 256): fold level-1 tables, entry (a, p) at
+//                   128 + (4a + p) * 4 = shift(b << 8p, 64a bytes), a = 1..7.
+//   [96, 160 KiB)   16 wave slots of 4 KiB: the segment being DMA'd in.
+//
+// Bank rule (ds_read_b32: lanes 0-31 and 32-63 are serviced separately,
+// bank = (address / 4) mod 32).  In lookup instruction j a lane reads the
+// table slot t = (j + q) & 3, q = (lane >> 3) & 3, replica r = lane & 7:
+// the 32 lanes of a half hit banks 8t + r -- all different, for any data.
+// The level-1 fold reads column 4a + t with a = 7 - (lane & 7), the
+// level-2 fold (lanes 8k only) column 4c + t: distinct banks again.
+// Each lookup address is ONE v_perm_b32 of (lane constant, data word,
+// per-lane selector): [const byte j, data byte t, 0, 0] = (byte << 8) | const.
+#pragma once
+#include <stdint.h>
+
+#include "gf2_crc32c.h"
+
+#if defined(__HIPCC__)
+#define WIPDB_LK_HD __host__ __device__
+#else
+#define WIPDB_LK_HD
+#endif
+
+namespace wipdb {
+namespace lk {
+
+constexpr int kWaves = 16;
+constexpr int kThreads = kWaves * 64;
+constexpr uint32_t kLdsL2 = 0;
+constexpr uint32_t kLdsMain = 32768;
+constexpr uint32_t kLdsSlots = 98304;
+constexpr uint32_t kSlotBytes = 4096;
+constexpr uint32_t kLdsBytes = kLdsSlots + kWaves * kSlotBytes;  // 160 KiB
+constexpr uint32_t kImageBytes = kLdsSlots;                    // tables + misc
+constexpr uint32_t kSegChunks = 256;                           // 16-B chunks per segment
+
+// misc word i (i < 1024) lives in the c = 0 column of level-2 row i / 4
+WIPDB_LK_HD constexpr uint32_t MiscAddr(uint32_t i) {
+  return (i >> 2) * 128u + (i & 3u) * 4u;
+}
+constexpr uint32_t kMiscInvTop = 0;    // 256 words: inv_top[v] (gf2::Tables)
+constexpr uint32_t kMiscHead0 = 256;   // 16 words: ~0 * x^(-8h)
+constexpr uint32_t kMiscUnit = 272;    // the workgroup's unit counter
+constexpr uint32_t kMiscBytes = 1024 * 4;
+
+// Flags of a launch (the HCRC_MASK_OUTPUT value is shared with the C-ABI).
+constexpr uint32_t kFlagMask = 0x2;
+// leave spans of at most kSmallMax bytes to the small-span path
+constexpr uint32_t kFlagSkipSmall = 0x4;
+// stop a span after its first segment when the rest is 16..kSmallMax bytes
+// (its unmasked partial CRC goes to out[i]); the small-span path finishes it
+constexpr uint32_t kFlagSplitRem = 0x8;
+constexpr uint32_t kSmallMax = 1024;
+
+// The remainder rule (shared by the kernels and the partition pass): a span
+// of n bytes at address a is cut after its first segment (4096 - a % 16
+// bytes) when what follows is 16..kSmallMax bytes.
+WIPDB_LK_HD constexpr uint32_t SplitRemainder(uint64_t a, uint32_t n) {
+  return (n > kSmallMax && n > 4096u - static_cast<uint32_t>(a & 15u) + 15u &&
+          n - (4096u - static_cast<uint32_t>(a & 15u)) <= kSmallMax)
+             ? 4096u - static_cast<uint32_t>(a & 15u)
+             : 0u;
+}
+
+// Builds the 96 KiB LDS image (tables + misc words; counters 0).
+inline void BuildLdsImage(uint32_t* img) {
+  using namespace wipdb::gf2;
+  Tables T;  // ~9 KiB on the caller's stack, built once per context
+  BuildTables(&T);
+  for (uint32_t i = 0; i < kImageBytes / 4; ++i) img[i] = 0;
+  uint32_t sh[4][256];
+  for (int c = 1; c < 8; ++c) {
+    BuildShiftTable(uint64_t(512) * c, sh);
+    for (int p = 0; p < 4; ++p)
+      for (int b = 0; b < 256; ++b) img[(kLdsL2 + b * 128 + (c * 4 + p) * 4) / 4] = sh[p][b];
+  }
+  for (int b = 0; b < 256; ++b)
+    for (int t = 0; t < 4; ++t)
+      for (int r = 0; r < 8; ++r) img[(kLdsMain + b * 256 + t * 32 + r * 4) / 4] = T.t[3 - t][b];
+  for (int a = 1; a < 8; ++a) {
+    BuildShiftTable(uint64_t(64) * a, sh);
+    for (int p = 0; p < 4; ++p)
+      for (int b = 0; b < 256; ++b)
+        img[(kLdsMain + b * 256 + 128 + (a * 4 + p) * 4) / 4] = sh[p][b];
+  }
+  for (int v = 0; v < 256; ++v) img[MiscAddr(kMiscInvTop + v) / 4] = T.inv_top[v];
+  for (int h = 0; h < 16; ++h) img[MiscAddr(kMiscHead0 + h) / 4] = T.head0[h];
+}
+
+}  // namespace lk
+}  // namespace wipdb

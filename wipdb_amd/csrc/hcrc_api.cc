@@ -19,6 +19,7 @@
 
 #include "../../include/hip_crc32c_batch.h"
 #include "crc32c_device.h"
+#include "crc32c_lds.h"
 #include "gf2_crc32c.h"
 
 namespace wipdb {
@@ -50,6 +51,16 @@ template <int SGT>
 __global__ void crc32c_small_kernel(const uint8_t*, SmallList, uint32_t*, uint32_t,
                                     const DevTables*, uint8_t*);
 }  // namespace dev
+namespace lk {
+__global__ void crc32c_lds_spans_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
+                                        const uint32_t*, uint32_t*, uint64_t, uint32_t,
+                                        const uint8_t*);
+__global__ void crc32c_lds_strided_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t,
+                                          uint32_t*, uint64_t, uint32_t, const uint8_t*);
+__global__ void crc32c_lds_verify_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
+                                         uint8_t*, uint64_t, uint32_t, uint32_t*,
+                                         const uint8_t*);
+}  // namespace lk
 }  // namespace wipdb
 
 using wipdb::dev::DevTables;
@@ -95,7 +106,8 @@ struct hcrc_ctx {
   hipMemPool_t scratch_pool = nullptr;
   int device = -1;
   hipStream_t stream = nullptr;
-  DevTables* d_tab = nullptr;
+  DevTables* d_tab = nullptr;      // small-span kernel tables
+  uint8_t* d_image = nullptr;       // LDS image of the LDS-staged kernels (crc32c_lds.h)
   int num_cu = 0;
   std::mutex mu;
   Slot slots[2];
@@ -183,23 +195,24 @@ struct WorkPool {
 // The kernels keep span indices in 32 bits: larger batches go in pieces.
 constexpr size_t kMaxLaunchSpans = size_t(1) << 31;
 
+// LDS-staged kernels: one workgroup per CU, but no more than the batch's
+// 16-span blocks (a workgroup's units are blocks w, w + grid, ...).
+int LdsGrid(hcrc_ctx* ctx, size_t count) {
+  const size_t need = (count + 15) / 16;
+  return static_cast<int>(std::max<size_t>(std::min<size_t>(need, size_t(ctx->num_cu)), 1));
+}
+
 int LaunchSpansKernel(hcrc_ctx* ctx, const void* base, const uint64_t* off,
                       const uint32_t* len, const uint32_t* init, uint32_t* out,
                       size_t count, uint32_t kflags, hipStream_t st) {
   for (size_t pos = 0; pos < count; pos += kMaxLaunchSpans) {
     const size_t n = std::min(count - pos, kMaxLaunchSpans);
-    WorkPool wp;
-    int rc = wp.Acquire(ctx, st);
-    if (rc != HCRC_OK) return rc;
-    hipLaunchKernelGGL(wipdb::dev::crc32c_spans_kernel, dim3(LaunchGrid(ctx, n)),
-                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+    hipLaunchKernelGGL(wipdb::lk::crc32c_lds_spans_kernel, dim3(LdsGrid(ctx, n)),
+                       dim3(wipdb::lk::kThreads), wipdb::lk::kLdsBytes, st,
                        static_cast<const uint8_t*>(base), off + pos, len + pos,
                        init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n), kflags,
-                       ctx->d_tab, wp.p);
-    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
-    const int rr = wp.Release(st);
-    if (rc == HCRC_OK) rc = rr;
-    if (rc != HCRC_OK) return rc;
+                       ctx->d_image);
+    if (hipGetLastError() != hipSuccess) return HCRC_ERR_LAUNCH;
   }
   return HCRC_OK;
 }
@@ -582,6 +595,16 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
     HCRC_CHECK(hipMemPoolSetAttribute(ctx->scratch_pool, hipMemPoolAttrReleaseThreshold, &keep));
   }
   const unsigned lds = wipdb::dev::kLdsBytes;
+  static_assert(wipdb::lk::kLdsBytes == wipdb::dev::kLdsBytes, "both kernel families use 160 KiB");
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::lk::crc32c_lds_spans_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::lk::crc32c_lds_strided_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HCRC_CHECK(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wipdb::lk::crc32c_lds_verify_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   HCRC_CHECK(hipFuncSetAttribute(
       reinterpret_cast<const void*>(wipdb::dev::crc32c_spans_kernel),
       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -605,6 +628,12 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
   HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_tab), sizeof(DevTables)));
   HCRC_CHECK(hipMemcpy(ctx->d_tab, ht.get(), sizeof(DevTables),
                        hipMemcpyHostToDevice));
+  {
+    std::vector<uint32_t> img(wipdb::lk::kImageBytes / 4);
+    wipdb::lk::BuildLdsImage(img.data());
+    HCRC_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), wipdb::lk::kImageBytes));
+    HCRC_CHECK(hipMemcpy(ctx->d_image, img.data(), wipdb::lk::kImageBytes, hipMemcpyHostToDevice));
+  }
   *out_ctx = ctx.release();
   return HCRC_OK;
 }
@@ -640,6 +669,7 @@ int hcrc_ctx_destroy(hcrc_ctx* ctx) {
     (void)hipFree(b.p);
   }
   if (ctx->d_tab) (void)hipFree(ctx->d_tab);
+  if (ctx->d_image) (void)hipFree(ctx->d_image);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->scratch_pool) {
     (void)hipDeviceSynchronize();
@@ -700,18 +730,12 @@ int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
   const hipStream_t st = StreamOf(ctx, stream);
   for (size_t pos = 0; pos < count; pos += kMaxLaunchSpans) {
     const size_t n = std::min(count - pos, kMaxLaunchSpans);
-    WorkPool wp;
-    int rc = wp.Acquire(ctx, st);
-    if (rc != HCRC_OK) return rc;
-    hipLaunchKernelGGL(wipdb::dev::crc32c_strided_kernel, dim3(LaunchGrid(ctx, n)),
-                       dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st,
+    hipLaunchKernelGGL(wipdb::lk::crc32c_lds_strided_kernel, dim3(LdsGrid(ctx, n)),
+                       dim3(wipdb::lk::kThreads), wipdb::lk::kLdsBytes, st,
                        static_cast<const uint8_t*>(d_base) + pos * stride, stride, length,
                        init_crc, d_out_crcs + pos, static_cast<uint64_t>(n),
-                       static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_tab, wp.p);
-    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
-    const int rr = wp.Release(st);
-    if (rc == HCRC_OK) rc = rr;
-    if (rc != HCRC_OK) return rc;
+                       static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_image);
+    if (hipGetLastError() != hipSuccess) return HCRC_ERR_LAUNCH;
   }
   return HCRC_OK;
 }
@@ -743,16 +767,10 @@ int LaunchVerify(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
     }
   }
   if (rc == HCRC_OK) {
-    WorkPool wp;
-    rc = wp.Acquire(ctx, st);
-    if (rc == HCRC_OK) {
-      hipLaunchKernelGGL(wipdb::dev::crc32c_verify_kernel, dim3(LaunchGrid(ctx, n)),
-                         dim3(wipdb::dev::kThreads), wipdb::dev::kLdsBytes, st, base, off, len,
-                         status, static_cast<uint64_t>(n), ctx->d_tab, wp.p, kflags, partial);
-      rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
-      const int rr = wp.Release(st);
-      if (rc == HCRC_OK) rc = rr;
-    }
+    hipLaunchKernelGGL(wipdb::lk::crc32c_lds_verify_kernel, dim3(LdsGrid(ctx, n)),
+                       dim3(wipdb::lk::kThreads), wipdb::lk::kLdsBytes, st, base, off, len,
+                       status, static_cast<uint64_t>(n), kflags, partial, ctx->d_image);
+    rc = hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH;
   }
   if (split && rc == HCRC_OK)
     rc = LaunchSmall(ctx, base, sl, tl, partial, wipdb::dev::kFlagVerify, status, st);
