@@ -1,28 +1,39 @@
 #!/usr/bin/env python3
 """Headline benchmark: device-resident GiB/s of batched CRC32C over 4 KiB
-blocks on 1..8 MI355X (BASELINE.json metric, configs[1] per GPU).
+blocks on 1..8 MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 A "step" is one launch of the batch entry point (hcrc_batch_async, the
-descriptor path a table builder would use) over this rank's whole shard:
-1 M blocks x 4 KiB (4 GiB) already resident in HBM, generated on device with
-a seeded splitmix64 stream (so the host can regenerate any block).  Weak
-scaling: every rank has its own 1 M-block shard; there is no data-path
+descriptor path a table builder would use) over this rank's whole shard of
+4 KiB blocks already resident in HBM, generated on device with a seeded
+splitmix64 stream.  N = 1: 1 M blocks (4 GiB, BASELINE configs[1]);
+N > 1: 8 M blocks (32 GiB) per rank, i.e. configs[3]'s 64 M x 4 KiB over 8
+GPUs.  Weak scaling: every rank has its own shard; there is no data-path
 collective (blocks are independent) -- only the barrier and the max-time
 reduction of the contract.  value = total bytes of all ranks / max time.
+
+Before the W warmup steps the bench preconditions the card with untimed
+launches of the same step (at least --precondition-ms of GPU time, 40 by
+default) and checks that every one of them returns the same CRCs: right
+after idle, back-to-back launches of this kernel run up to 1.5x slower for
+the first ~30-40 ms while the SMU settles the power-capped clocks
+(profiles/r02_launch_series.json); the timed steps measure the steady state.
+The line says so ("precondition").
 
 Also printed in the same JSON line:
   roofline      the CRC kernel's average launch time from HIP events on the
                 launch stream; achieved = algorithmic bytes per launch
                 (4096 + 4 per block) / that time, vs the 8 TB/s HBM peak;
                 traffic = PMC HBM bytes per launch from the committed rocprof
-                profile of this config (profiles/), or null.
+                profile of this config (profiles/traffic.json), or null.
   cpu_baseline  the reference kv::crc32c (oracle/_ref, compiled from the
-                reference's own sources) on this host, 1 thread, over a
-                bounded sample of the same blocks; rank 0, N=1 only.
-  parity        the sample's reference CRCs vs the GPU's for the same blocks.
+                reference's own sources) on this host, 1 thread, over the
+                shard's blocks copied back from HBM (config 1's 4 GiB from
+                DRAM), and on every CPU this process may use; rank 0, N=1.
+  parity        the reference CRCs vs the GPU's for every block of the shard
+                (N = 1) or a 64 Ki-block sample per rank (N > 1).
 """
 from __future__ import annotations
 
@@ -47,74 +58,81 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)  # >= 50 back-to-back launches
-    # the first ~20 back-to-back launches of a fresh process run 5-15 % slow
-    # while the card's clocks settle under sustained load
-    # (scripts/launch_series.py): the default warmup
-    # covers them, so the timed steps see the steady state
-    p.add_argument("--warmup", type=int, default=30)
-    p.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--precondition-ms", type=float, default=40.0,
+                   help="untimed GPU time of same-step launches before the warmup (power "
+                        "transient, see the docstring); 0 disables")
+    p.add_argument("--blocks", type=int, default=0,
+                   help="blocks per GPU (default: 1 M at N = 1, 8 M per rank at N > 1)")
     p.add_argument("--mode", choices=["spans", "strided"], default="spans")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=10.0,
-                   help="target CPU time of the reference baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=5.0,
+                   help="minimum time of the 1-thread reference baseline (whole passes)")
     p.add_argument("--readstream", action="store_true",
                    help="also time the read-stream ceiling kernel")
-    p.add_argument("--stride", type=int, default=BLOCK,
-                   help="diagnostic: block stride (0 = every block reads the same 4 KiB, "
-                        "i.e. cache-resident compute ceiling); the headline uses 4096")
-    p.add_argument("--len", type=int, default=BLOCK, choices=range(0, 65537), metavar="0..65536",
-                   help="diagnostic: bytes CRC'd per block (<= stride; e.g. 4092 = a 4 KiB "
-                        "on-disk block minus its 5-byte trailer, plus the type byte)")
-    p.add_argument("--fill", choices=["splitmix", "zero"], default="splitmix",
-                   help="diagnostic: block contents (zero = low-toggle data, to probe "
-                        "the power/clock limit); the headline uses splitmix")
-    p.add_argument("--order", choices=["natural", "group", "cu"], default="natural",
-                   help="diagnostic: which block each descriptor names (natural: block i; "
-                        "group: every lane group sweeps its own contiguous run; cu: every "
-                        "workgroup sweeps its own contiguous region)")
     return p.parse_args()
 
 
-def cpu_baseline(seed, blocks_on_gpu_crc, first_block, target_s):
-    """Reference kv::crc32c on this host over a bounded sample of rank 0's
-    blocks (regenerated from the seed), 1 thread; plus the parity check of
-    those CRCs against the GPU's."""
-    import numpy as np
-    from tests.golden.common import splitmix64_bytes
+def _ref_batch():
+    """The reference kv::crc32c batch driver (oracle/_ref, compiled from the
+    reference's own sources), or the oracle restatement (a port)."""
     ref_path = os.path.join(REPO, "oracle", "_ref", "libref_crc32c.so")
-    kind = "reference"
     if os.path.exists(ref_path):
         lib = ctypes.CDLL(ref_path)
         fn = lib.ref_crc32c_batch
         fn.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
-    else:  # fall back to the oracle restatement (a port), still a CPU baseline
-        kind = "port"
-        lib = ctypes.CDLL(os.path.join(REPO, "oracle", "_build", "liboracle.so"))
-        ofn = lib.oracle_crc32c_batch
-        ofn.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int]
+        return fn, "reference"
+    lib = ctypes.CDLL(os.path.join(REPO, "oracle", "_build", "liboracle.so"))
+    ofn = lib.oracle_crc32c_batch
+    ofn.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int]
 
-        def fn(b, o, l, i, out, n, m, t):  # noqa: E741
-            ofn(b, o, l, i, out, n, m)
-    nblk = 1 << 16  # 64 Ki blocks = 256 MiB sample
-    buf = splitmix64_bytes(seed, nblk * BLOCK, start=first_block * BLOCK)
-    offs = (np.arange(nblk, dtype=np.uint64) * BLOCK)
+    def fn(b, o, l, i, out, n, m, t):  # noqa: E741
+        ofn(b, o, l, i, out, n, m)
+    return fn, "port"
+
+
+def usable_cpus() -> int:
+    """CPUs this process may use: the affinity mask, capped by the job's CPU
+    share when the launcher states one (OMP_NUM_THREADS; the GPU box gives a
+    one-GPU job 16 of the host's 256 CPUs)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        share = 0
+    return min(n, share) if share > 0 else n
+
+
+def cpu_check(host_blocks, gpu_crc, target_s, baseline: bool):
+    """Reference CRCs of every given block (all usable CPUs) vs the GPU's;
+    with `baseline`, also the reference's rate on 1 thread (whole passes
+    over the blocks, at least target_s) and on all usable CPUs."""
+    import numpy as np
+    fn, kind = _ref_batch()
+    nblk = host_blocks.size // BLOCK
+    offs = np.arange(nblk, dtype=np.uint64) * BLOCK
     lens = np.full(nblk, BLOCK, np.uint32)
     out = np.empty(nblk, np.uint32)
-    args = (buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, out.ctypes.data)
-    fn(*args, nblk, 0, 1)  # warm
+    args = (host_blocks.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, out.ctypes.data)
+    ncpu = usable_cpus()
+    t0 = time.perf_counter()
+    fn(*args, nblk, 0, ncpu)
+    all_s = time.perf_counter() - t0
+    mism = int((out != gpu_crc[:nblk]).sum())
+    parity = {"blocks_checked": int(nblk), "mismatches": mism}
+    if not baseline:
+        return None, parity
     passes, t0 = 0, time.perf_counter()
     while True:
         fn(*args, nblk, 0, 1)
         passes += 1
         el = time.perf_counter() - t0
-        if el >= target_s or passes >= 400:
+        if el >= target_s:
             break
     gib_s = passes * nblk * BLOCK / el / 2**30
-    mism = int((out != blocks_on_gpu_crc[:nblk]).sum())
-    t16, tt0 = 16, time.perf_counter()
-    fn(*args, nblk, 0, t16)
-    fn(*args, nblk, 0, t16)
-    all_gib = 2 * nblk * BLOCK / (time.perf_counter() - tt0) / 2**30
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -126,11 +144,15 @@ def cpu_baseline(seed, blocks_on_gpu_crc, first_block, target_s):
         pass
     return {
         "value": round(gib_s, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
-        "sample": f"{nblk} x 4 KiB blocks (256 MiB) of rank 0's shard regenerated on the host, "
-                  f"{passes} passes ({el:.1f} s), ref kv::crc32c::Extend per block",
-        "all_cores": {"value": round(all_gib, 3), "cores": t16},
-        "host": {"cpu": cpu_model, "nproc": os.cpu_count(), "hostname": socket.gethostname()},
-    }, {"blocks_checked": nblk, "mismatches": mism}
+        "sample": f"all {nblk} x 4 KiB blocks of rank 0's shard ({nblk * BLOCK >> 20} MiB, "
+                  f"copied back from HBM, read from DRAM), {passes} pass(es) in {el:.1f} s, "
+                  f"ref kv::crc32c::Extend per block",
+        "all_cores": {"value": round(nblk * BLOCK / all_s / 2**30, 3), "cores": ncpu,
+                      "note": "one pass over the same blocks on every CPU this job may use "
+                              "(affinity mask capped by OMP_NUM_THREADS)"},
+        "host": {"cpu": cpu_model, "nproc": os.cpu_count(), "usable_cpus": ncpu,
+                 "hostname": socket.gethostname()},
+    }, parity
 
 
 def committed_traffic(mode: str, blocks: int):
@@ -143,6 +165,9 @@ def committed_traffic(mode: str, blocks: int):
         return None if e is None else e.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+KERNEL = {"spans": "crc32c_lds_spans_kernel", "strided": "crc32c_lds_strided_kernel"}
 
 
 def main():
@@ -162,41 +187,45 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    blocks = a.blocks or ((1 << 20) if world == 1 else (8 << 20))
 
     eng = Engine(local)
-    first, nblk = block_shard(rank, world, a.blocks)  # weak scaling, no collective
-    # diagnostic spans longer than the 4 KiB pitch (--len > 4096) or a wider
-    # --stride run past nblk * 4 KiB: size the buffer so every span stays
-    # inside the allocation
-    need = max(nblk * BLOCK, (nblk - 1) * max(a.stride, 0) + a.len)
-    data = torch.empty((need + 4095) // 4096 * 4096, dtype=torch.uint8, device=dev)
+    first, nblk = block_shard(rank, world, blocks)  # weak scaling, no collective
+    data = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    if a.fill == "zero":
-        data.zero_()
-    else:
-        eng.fill_splitmix64_device(data, SEED, first_word=first * BLOCK // 8,
-                                   stream=stream.cuda_stream)
-    idx = torch.arange(nblk, dtype=torch.int64, device=dev)
-    if a.order != "natural":
-        # span s is taken by lane group q = s % G at step k = s // G of the
-        # persistent grid (G = groups in the grid)
-        G = torch.cuda.get_device_properties(dev).multi_processor_count * 16 * 2
-        assert nblk % G == 0, "diagnostic orders need blocks divisible by the grid's groups"
-        q, k = idx % G, idx // G
-        if a.order == "group":
-            idx = q * (nblk // G) + k
-        else:
-            per_wg = 2 * 16  # groups per workgroup
-            idx = (q // per_wg) * (nblk // (G // per_wg)) + k * per_wg + q % per_wg
-    offs = idx * a.stride
-    lens = torch.full((nblk,), a.len, dtype=torch.int32, device=dev)
+    eng.fill_splitmix64_device(data, SEED, first_word=first * BLOCK // 8, stream=stream.cuda_stream)
+    offs = torch.arange(nblk, dtype=torch.int64, device=dev) * BLOCK
+    lens = torch.full((nblk,), BLOCK, dtype=torch.int32, device=dev)
     out = torch.empty(nblk, dtype=torch.int32, device=dev)
 
-    def step():
+    def step(dst=out):
         if a.mode == "spans":
-            eng.batch_device(data, offs, lens, None, out, stream=stream.cuda_stream)
+            eng.batch_device(data, offs, lens, None, dst, stream=stream.cuda_stream)
         else:
-            eng.batch_strided_device(data, a.stride, BLOCK, nblk, 0, out, stream=stream.cuda_stream)
+            eng.batch_strided_device(data, BLOCK, BLOCK, nblk, 0, dst, stream=stream.cuda_stream)
+
+    # precondition: untimed launches of the step, every output equal to the first
+    pre = {"launches": 0, "gpu_ms": 0.0, "identical_outputs": True}
+    if a.precondition_ms > 0:
+        ref = torch.empty_like(out)
+        step(ref)
+        scratch = torch.empty_like(out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        n = 0
+        while True:
+            for _ in range(8):
+                step(scratch)
+                n += 1
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            pre["identical_outputs"] &= bool(torch.equal(scratch, ref))
+            if e0.elapsed_time(e1) >= a.precondition_ms or n >= 4096:
+                break
+        pre["launches"] = n + 1
+        pre["gpu_ms"] = round(e0.elapsed_time(e1), 2)
+        pre["why"] = ("after idle, back-to-back launches run up to 1.5x slower for ~30-40 ms while "
+                      "the SMU settles the power-capped clocks (profiles/r02_launch_series.json)")
 
     for _ in range(a.warmup):
         step()
@@ -216,7 +245,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sorted(s.elapsed_time(e) for s, e in ev)
+    kern_ms = [s.elapsed_time(e) for s, e in ev]
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
     elapsed_max = max_over_ranks(elapsed, dev)
@@ -237,10 +266,25 @@ def main():
         rs = {"kernel": "readstream_kernel", "avg_ms": round(rs_ms, 4),
               "read_GBps": round(nblk * BLOCK / rs_ms / 1e6, 1)}
 
+    # parity (and, rank 0 at N = 1, the CPU baseline) on the host
+    gpu_crc = out.cpu().numpy().view(np.uint32)
+    full = world == 1
+    nchk = nblk if full else min(nblk, 1 << 16)
+    host_blocks = data[: nchk * BLOCK].cpu().numpy()
+    cb, par = cpu_check(host_blocks, gpu_crc, a.cpu_seconds,
+                        baseline=(rank == 0 and world == 1 and not a.no_cpu_baseline))
+    del host_blocks
+    if world > 1:
+        t = torch.tensor([par["mismatches"], par["blocks_checked"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        par = {"blocks_checked": int(t[1].item()), "mismatches": int(t[0].item()),
+               "scope": "64 Ki-block sample per rank"}
+
     if rank == 0:
         total_bytes = world * nblk * BLOCK
         value = total_bytes * a.steps / elapsed_max / 2**30
         achieved = nblk * ALGO_BYTES_PER_BLOCK / (kern_avg_ms * 1e-3) / 1e9
+        cfg = "BASELINE configs[1]" if world == 1 else "BASELINE configs[3]: 8 M blocks per GPU"
         line = {
             "metric": "device-resident GiB/s, batched CRC32C of 4 KiB blocks, 1/2/4/8 MI355X",
             "value": round(value, 2),
@@ -255,38 +299,25 @@ def main():
             "dtype": "u8",
             "data": "synthetic (device-generated splitmix64, seed 0x4B10C5)",
             "config": {"workload": f"{nblk} x 4 KiB blocks per GPU, device-resident "
-                                   f"(BASELINE configs[1]); {a.mode} entry point",
+                                   f"({cfg}); {a.mode} entry point",
                        "blocks_per_gpu": nblk, "block_bytes": BLOCK,
                        "parallelism": f"shard{world} (independent blocks, no collective)"},
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": committed_traffic(a.mode, nblk),
-                "kernel": "crc32c_spans_kernel" if a.mode == "spans" else "crc32c_strided_kernel",
+                "kernel": KERNEL[a.mode],
                 "kernel_avg_ms": round(kern_avg_ms, 4),
+                "kernel_min_ms": round(min(kern_ms), 4),
                 "algorithmic_bytes_per_launch": nblk * ALGO_BYTES_PER_BLOCK,
             },
+            "precondition": pre,
         }
         if rs:
             line["readstream_ceiling"] = rs
-        if a.len != BLOCK:
-            line["config"]["diagnostic_len"] = a.len
-            line["metric"] += " [DIAGNOSTIC len]"
-        if a.fill != "splitmix":
-            line["config"]["diagnostic_fill"] = a.fill
-            line["metric"] += " [DIAGNOSTIC fill]"
-        if a.order != "natural":
-            line["config"]["diagnostic_order"] = a.order
-            line["metric"] += " [DIAGNOSTIC order]"
-        if a.stride != BLOCK:
-            line["config"]["diagnostic_stride"] = a.stride
-            line["metric"] += " [DIAGNOSTIC stride, not the headline]"
-        if (world == 1 and not a.no_cpu_baseline and a.stride == BLOCK and a.fill == "splitmix"
-                and a.len == BLOCK):
-            gpu_crc = out.cpu().numpy().view(np.uint32)
-            cb, par = cpu_baseline(SEED, gpu_crc, first, a.cpu_seconds)
+        if cb:
             line["cpu_baseline"] = cb
-            line["parity"] = par
+        line["parity"] = par
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -20,7 +20,7 @@
  *   hcrc_verify_async, hcrc_verify_async_ex
  *       ReadBlock's check (kv/src/table/format.cc:91-99):
  *       Unmask(stored) == Value(data, n+1) for a batch of blocks.
- *   hcrc_batch_multi
+ *   hcrc_batch_multi, hcrc_batch_multi_ex
  *       a batch sharded by bytes over several GPUs of one node (no
  *       collective: blocks are independent).
  *   hcrc_cpu_extend / hcrc_cpu_batch
@@ -41,9 +41,14 @@
  * entry points never fall back to the CPU silently; a caller that wants a
  * fallback (the C++ wrapper's AUTO policy) calls hcrc_cpu_batch itself.
  *
- * Threading: a context may be used from several threads; calls on one
- * context are serialised by an internal mutex (async calls on
- * caller-provided streams only hold it while enqueueing).
+ * Threading (the reference's flush, compaction and split pools call
+ * Extend concurrently, kv/tests/db/kv_bench.cc:2041-2043): a context may be
+ * used from any number of threads at once.  The async entry points take no
+ * lock (they only enqueue on the caller's stream); a synchronous call
+ * (hcrc_batch, hcrc_batch_multi) leases one of up to 8 per-context lanes --
+ * its own HIP stream and pinned staging slots -- so concurrent calls overlap
+ * on the device.  Every entry point leaves the caller's current HIP device
+ * as it found it.
  */
 #ifndef HIP_CRC32C_BATCH_H_
 #define HIP_CRC32C_BATCH_H_
@@ -70,15 +75,15 @@ extern "C" {
 #define HCRC_HOST_PTRS 0x0    /* all array/data pointers are host memory    */
 #define HCRC_DEVICE_PTRS 0x1  /* all array/data pointers are device memory  */
 #define HCRC_MASK_OUTPUT 0x2  /* write Mask(crc) instead of crc             */
-/* Spans of at most 1024 bytes are checksummed by the small-span kernel
- * (8 per wave slot) instead of a whole 4 KiB group segment each, and so are
- * the last 16..1024 bytes of a span that just overruns one 4 KiB segment (a
- * table block: 4096 bytes + its last entry + the type byte): the spans
- * kernel stops after the first segment and the small kernel continues from
- * its partial CRC.  A partition pass compacts them, stream-ordered scratch
- * (hipMallocAsync).  Same results; pays off for batches with many short
- * spans (WAL records, small meta blocks) or table blocks.  hcrc_batch on
- * host memory chooses it by itself.  count < 2^31 per call. */
+/* Size classes: a partition pass sorts the batch into spans of at most
+ * ~1 KiB (checksummed 4 per wave iteration), at most ~2 KiB (2 per wave
+ * iteration) and longer ones (a wave per 4 KiB segment); a span that just
+ * overruns its first 4 KiB segment by up to 2 KiB (a table block: 4096
+ * bytes + its last entry + the type byte) is cut there and its remainder
+ * continues from the partial CRC in the small classes.  Same results; pays
+ * off for batches with many short spans (WAL records, small meta blocks) or
+ * table blocks.  hcrc_batch on host memory chooses it by itself.  Uses
+ * stream-ordered scratch (~64 bytes per span). */
 #define HCRC_SPLIT_SMALL 0x4
 
 typedef struct hcrc_ctx hcrc_ctx;
@@ -125,10 +130,10 @@ int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base,
 int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base,
                       const uint64_t* d_offsets, const uint32_t* d_lengths,
                       uint8_t* d_status, size_t count, void* stream);
-/* The same with flags: 0 or HCRC_SPLIT_SMALL (blocks of at most 1 KiB, and
- * the last 16..1024 bytes of blocks that just overrun 4 KiB -- a table's
- * data blocks are 4 KiB plus their last entry -- go to the small-span
- * kernel).  count < 2^31 per call with HCRC_SPLIT_SMALL. */
+/* The same with flags: 0 or HCRC_SPLIT_SMALL (the size classes above:
+ * small blocks several per wave iteration, a table's data blocks -- 4 KiB
+ * plus their last entry -- cut after their first 4 KiB and finished in the
+ * small classes). */
 int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base,
                          const uint64_t* d_offsets, const uint32_t* d_lengths,
                          uint8_t* d_status, size_t count, int flags, void* stream);
@@ -142,12 +147,21 @@ int hcrc_batch_multi(const int* devices, int ndev, const void* base,
                      const uint64_t* offsets, const uint32_t* lengths,
                      const uint32_t* init_crcs, uint32_t* out_crcs,
                      size_t count, int flags);
+/* The same, with each shard's own return code in shard_rc[ndev] (nullable):
+ * a failing device fails its shard only; the return value is the first
+ * non-zero shard code.  A device may be listed more than once (its shards
+ * then run concurrently on one shared context). */
+int hcrc_batch_multi_ex(const int* devices, int ndev, const void* base,
+                        const uint64_t* offsets, const uint32_t* lengths,
+                        const uint32_t* init_crcs, uint32_t* out_crcs,
+                        size_t count, int flags, int* shard_rc);
 
-/* Pinned host memory.  hcrc_batch over spans that lie in pinned memory
- * (hcrc_host_alloc) or in a registered range (hcrc_host_register: e.g. an
+/* Pinned host memory.  hcrc_batch over spans that all lie in ONE range
+ * allocated by hcrc_host_alloc or registered by hcrc_host_register (e.g. an
  * mmap'd SST file or a long-lived memtable arena) runs zero-copy: the kernel
- * reads the spans over PCIe directly, with no staging copy (~1.6x the
- * staged rate).  Pageable memory goes through the pinned staging slots. */
+ * reads the spans over PCIe directly, with no staging copy.  Anything else
+ * (pageable memory, memory pinned by other means, spans spread over several
+ * ranges) goes through the pinned staging slots. */
 int hcrc_host_alloc(size_t bytes, void** out_ptr);
 int hcrc_host_free(void* ptr);
 int hcrc_host_register(void* ptr, size_t bytes);

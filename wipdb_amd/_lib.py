@@ -54,6 +54,9 @@ _PROTOS = {
     "hcrc_sync": (_c.c_int, [_vp, _vp]),
     "hcrc_batch_multi": (
         _c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _vp, _vp, _vp, _vp, _vp, _sz, _c.c_int]),
+    "hcrc_batch_multi_ex": (
+        _c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _vp, _vp, _vp, _vp, _vp, _sz, _c.c_int,
+                   _c.POINTER(_c.c_int)]),
     "hcrc_host_alloc": (_c.c_int, [_sz, _c.POINTER(_vp)]),
     "hcrc_host_free": (_c.c_int, [_vp]),
     "hcrc_host_register": (_c.c_int, [_vp, _sz]),

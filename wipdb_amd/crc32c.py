@@ -92,6 +92,32 @@ def device_count() -> int:
 # --------------------------------------------------------------------------
 # batch engine (GPU)
 # --------------------------------------------------------------------------
+def _check_tensor(t, name: str, device, dtypes, min_numel: int = 0) -> None:
+    """Device tensor arguments are raw pointers at the C-ABI: a wrong dtype
+    (e.g. torch's default int64 for a u32 column), a strided view or a tensor
+    on another device would be read as garbage or out of bounds by the
+    kernel, so they are rejected here."""
+    if t is None:
+        return
+    if not hasattr(t, "data_ptr"):
+        raise TypeError(f"{name}: expected a torch tensor")
+    if t.device != device:
+        raise ValueError(f"{name}: on {t.device}, the engine's device is {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if dtypes is not None and t.dtype not in dtypes:
+        raise TypeError(f"{name}: dtype {t.dtype}, expected one of {[str(d) for d in dtypes]}")
+    if t.numel() < min_numel:
+        raise ValueError(f"{name}: {t.numel()} elements, need {min_numel}")
+
+
+def _dtypes():
+    import torch
+    u32 = tuple(d for d in (torch.int32, getattr(torch, "uint32", None)) if d is not None)
+    u64 = tuple(d for d in (torch.int64, getattr(torch, "uint64", None)) if d is not None)
+    return u32, u64, (torch.uint8,)
+
+
 class Engine:
     """One hcrc context (device tables, stream, pinned staging) per GPU."""
 
@@ -146,16 +172,40 @@ class Engine:
             return int(stream.cuda_stream)
         return int(stream)
 
+    def _device(self):
+        import torch
+        return torch.device("cuda", self.device)
+
+    def _check_spans(self, base_t, offsets_t, lengths_t, inits_t, check_bounds: bool) -> int:
+        u32, u64, _ = _dtypes()
+        dev = self._device()
+        _check_tensor(base_t, "base", dev, None)
+        _check_tensor(offsets_t, "offsets", dev, u64)
+        n = int(offsets_t.numel())
+        _check_tensor(lengths_t, "lengths", dev, u32, n)
+        _check_tensor(inits_t, "inits", dev, u32, n)
+        if check_bounds and n:
+            import torch
+            end = offsets_t[:n].to(torch.int64) + lengths_t[:n].to(torch.int64).bitwise_and(0xFFFFFFFF)
+            nbytes = base_t.numel() * base_t.element_size()
+            if int(offsets_t[:n].min()) < 0 or int(end.max()) > nbytes:
+                raise ValueError("a span lies outside base")
+        return n
+
     def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
-                     mask_output: bool = False, stream=None, split_small: bool = False):
+                     mask_output: bool = False, stream=None, split_small: bool = False,
+                     check_bounds: bool = False):
         """Asynchronous batch on device tensors; returns the uint32 out tensor
         (int32 storage).  Enqueued on ``stream`` (default: torch's current).
-        ``split_small``: HCRC_SPLIT_SMALL (spans <= 1 KiB on the small-span
-        kernel)."""
+        ``split_small``: HCRC_SPLIT_SMALL (the size classes).  Offsets are
+        int64, lengths / inits / out 32-bit, all contiguous on this engine's
+        device; ``check_bounds`` also checks every span against base (a
+        device reduction and a sync)."""
         import torch
-        n = int(offsets_t.numel())
+        n = self._check_spans(base_t, offsets_t, lengths_t, inits_t, check_bounds)
         if out_t is None:
             out_t = torch.empty(n, dtype=torch.int32, device=base_t.device)
+        _check_tensor(out_t, "out", self._device(), _dtypes()[0], n)
         flags = HCRC_DEVICE_PTRS | (HCRC_MASK_OUTPUT if mask_output else 0)
         if split_small:
             flags |= HCRC_SPLIT_SMALL
@@ -167,8 +217,12 @@ class Engine:
     def batch_strided_device(self, base_t, stride: int, length: int, count: int, init: int = 0,
                              out_t=None, mask_output: bool = False, stream=None):
         import torch
+        _check_tensor(base_t, "base", self._device(), None)
+        if count and (count - 1) * stride + length > base_t.numel() * base_t.element_size():
+            raise ValueError("the strided blocks run past base")
         if out_t is None:
             out_t = torch.empty(count, dtype=torch.int32, device=base_t.device)
+        _check_tensor(out_t, "out", self._device(), _dtypes()[0], count)
         flags = HCRC_DEVICE_PTRS | (HCRC_MASK_OUTPUT if mask_output else 0)
         check(self._lib.hcrc_batch_strided_async(self._ctx, _ptr(base_t), stride, length,
                                                  init & 0xFFFFFFFF, _ptr(out_t), count, flags,
@@ -183,9 +237,10 @@ class Engine:
         HCRC_SPLIT_SMALL (small blocks and table-block remainders on the
         small-span kernel)."""
         import torch
-        n = int(offsets_t.numel())
+        n = self._check_spans(base_t, offsets_t, lengths_t, None, False)
         if status_t is None:
             status_t = torch.empty(n, dtype=torch.uint8, device=base_t.device)
+        _check_tensor(status_t, "status", self._device(), _dtypes()[2], n)
         check(self._lib.hcrc_verify_async_ex(self._ctx, _ptr(base_t), _ptr(offsets_t),
                                              _ptr(lengths_t), _ptr(status_t), n,
                                              HCRC_SPLIT_SMALL if split_small else 0,
@@ -216,8 +271,10 @@ class Engine:
 
 
 def batch_multi(devices: Sequence[int], base, offsets, lengths, inits=None,
-                mask_output: bool = False) -> np.ndarray:
-    """Host batch sharded by bytes over several GPUs (no collective)."""
+                mask_output: bool = False, shard_status: bool = False):
+    """Host batch sharded by bytes over several GPUs (no collective).  With
+    ``shard_status`` returns (out, per-shard return codes) without raising;
+    a device may be listed more than once."""
     lib = _lib.load()
     base = _as_bytes(base)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -225,9 +282,13 @@ def batch_multi(devices: Sequence[int], base, offsets, lengths, inits=None,
     ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
     out = np.empty(off.size, dtype=np.uint32)
     devs = (ctypes.c_int * len(devices))(*devices)
+    rcs = (ctypes.c_int * len(devices))()
     flags = HCRC_MASK_OUTPUT if mask_output else 0
-    check(lib.hcrc_batch_multi(devs, len(devices), _ptr(base), _ptr(off), _ptr(ln), _ptr(ini),
-                               _ptr(out), off.size, flags), "hcrc_batch_multi")
+    rc = lib.hcrc_batch_multi_ex(devs, len(devices), _ptr(base), _ptr(off), _ptr(ln), _ptr(ini),
+                                 _ptr(out), off.size, flags, rcs)
+    if shard_status:
+        return out, list(rcs)
+    check(rc, "hcrc_batch_multi_ex")
     return out
 
 

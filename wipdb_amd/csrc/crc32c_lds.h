@@ -59,22 +59,31 @@ constexpr uint32_t kMiscBytes = 1024 * 4;
 
 // Flags of a launch (the HCRC_MASK_OUTPUT value is shared with the C-ABI).
 constexpr uint32_t kFlagMask = 0x2;
-// leave spans of at most kSmallMax bytes to the small-span path
-constexpr uint32_t kFlagSkipSmall = 0x4;
-// stop a span after its first segment when the rest is 16..kSmallMax bytes
-// (its unmasked partial CRC goes to out[i]); the small-span path finishes it
-constexpr uint32_t kFlagSplitRem = 0x8;
-constexpr uint32_t kSmallMax = 1024;
 
-// The remainder rule (shared by the kernels and the partition pass): a span
-// of n bytes at address a is cut after its first segment (4096 - a % 16
-// bytes) when what follows is 16..kSmallMax bytes.
-WIPDB_LK_HD constexpr uint32_t SplitRemainder(uint64_t a, uint32_t n) {
-  return (n > kSmallMax && n > 4096u - static_cast<uint32_t>(a & 15u) + 15u &&
-          n - (4096u - static_cast<uint32_t>(a & 15u)) <= kSmallMax)
-             ? 4096u - static_cast<uint32_t>(a & 15u)
-             : 0u;
-}
+// Size classes (HCRC_SPLIT_SMALL).  A span of n bytes at address a covers
+// f = (a % 16 + n) / 16 full chunks of its 16-byte grid.  Class 4 (16-lane
+// groups, 4 spans per wave iteration): f <= 64; class 2 (32-lane groups):
+// f <= 128; class 1: the rest, segment by segment.  A class-1 span whose
+// chunks beyond its first 256 number 1..128 (a table block: 4 KiB + its last
+// entry + the type byte) is cut: the class-1 kernel writes the partial CRC
+// of its first 256 chunks and the remainder -- 16-aligned, so no head --
+// goes to class 2 or 4 as a continuation.
+constexpr uint32_t kClass4Chunks = 64;
+constexpr uint32_t kClass2Chunks = 128;
+constexpr uint32_t kListCut = 0x80000000u;   // id word: class-1 entry stops after its first segment
+constexpr uint32_t kListCont = 0x40000000u;  // id word: continues from the partial CRC of span id
+constexpr uint32_t kListIdMask = 0x3fffffffu;
+constexpr uint64_t kMaxListSpans = uint64_t(1) << 30;
+
+// One size-class list (struct of arrays, device memory); `count` is a device
+// counter the partition kernel fills.
+struct SpanList {
+  uint64_t* off;   // byte offset of the (remainder's) first byte from the batch base
+  uint32_t* len;   // bytes (verify: including the type byte)
+  uint32_t* init;  // init_crc (continuations: unused)
+  uint32_t* id;    // output slot | kListCut | kListCont
+  uint32_t* count;
+};
 
 // Builds the 96 KiB LDS image (tables + misc words; counters 0).
 inline void BuildLdsImage(uint32_t* img) {
