@@ -15,10 +15,10 @@ collective (blocks are independent) -- only the barrier and the max-time
 reduction of the contract.  value = total bytes of all ranks / max time.
 
 Before the W warmup steps the bench preconditions the card with untimed
-launches of the same step (at least --precondition-ms of GPU time, 40 by
+launches of the same step (at least --precondition-ms of GPU time, 80 by
 default) and checks that every one of them returns the same CRCs: right
 after idle, back-to-back launches of this kernel run up to 1.5x slower for
-the first ~30-40 ms while the SMU settles the power-capped clocks
+the first ~30-60 ms while the SMU settles the power-capped clocks
 (profiles/r02_launch_series.json); the timed steps measure the steady state.
 The line says so ("precondition").
 
@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)  # >= 50 back-to-back launches
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--precondition-ms", type=float, default=40.0,
+    p.add_argument("--precondition-ms", type=float, default=80.0,
                    help="untimed GPU time of same-step launches before the warmup (power "
                         "transient, see the docstring); 0 disables")
     p.add_argument("--blocks", type=int, default=0,
@@ -204,28 +204,31 @@ def main():
         else:
             eng.batch_strided_device(data, BLOCK, BLOCK, nblk, 0, dst, stream=stream.cuda_stream)
 
-    # precondition: untimed launches of the step, every output equal to the first
+    # precondition: untimed back-to-back launches of the step (at least
+    # precondition_ms of GPU time), every output compared with the first
     pre = {"launches": 0, "gpu_ms": 0.0, "identical_outputs": True}
     if a.precondition_ms > 0:
         ref = torch.empty_like(out)
-        step(ref)
         scratch = torch.empty_like(out)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        step(ref)
         e0.record(stream)
-        n = 0
-        while True:
-            for _ in range(8):
-                step(scratch)
-                n += 1
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            pre["identical_outputs"] &= bool(torch.equal(scratch, ref))
-            if e0.elapsed_time(e1) >= a.precondition_ms or n >= 4096:
-                break
-        pre["launches"] = n + 1
-        pre["gpu_ms"] = round(e0.elapsed_time(e1), 2)
-        pre["why"] = ("after idle, back-to-back launches run up to 1.5x slower for ~30-40 ms while "
-                      "the SMU settles the power-capped clocks (profiles/r02_launch_series.json)")
+        step(scratch)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        n = max(8, min(4096, int(a.precondition_ms / max(e0.elapsed_time(e1), 1e-3)) + 1))
+        mism = torch.zeros((), dtype=torch.int64, device=dev)
+        e0.record(stream)
+        for _ in range(n):
+            step(scratch)
+            mism += (scratch != ref).sum()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        pre = {"launches": n + 2, "gpu_ms": round(e0.elapsed_time(e1), 2),
+               "identical_outputs": int(mism.item()) == 0,
+               "why": "after idle, back-to-back launches run up to 1.5x slower for ~30-60 ms while "
+                      "the SMU settles the power-capped clocks (profiles/r02_launch_series.json)"}
+        del ref, scratch
 
     for _ in range(a.warmup):
         step()

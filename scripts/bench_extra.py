@@ -75,11 +75,33 @@ def check_sample(host, offs, lens, got, rng, k=4000):
 SPLIT = False  # --split: HCRC_SPLIT_SMALL on the device batches
 
 
+def batch_latency(eng, dbuf, do, dl, stream, nbatch_bytes=2 << 20, reps=200):
+    """p50 / p99 of synchronised SST-sized batches (~2 MiB of these spans per
+    launch, consecutive slices of the batch), host wall time."""
+    lens = dl.cpu().numpy().view(np.uint32).astype(np.int64)
+    per = max(1, int(np.searchsorted(np.cumsum(lens + 5), nbatch_bytes)))
+    n = lens.size
+    outs = torch.empty(per, dtype=torch.int32, device=dbuf.device)
+    lat = []
+    for i in range(reps + 20):
+        lo = (i * per) % max(1, n - per)
+        o_i, l_i = do[lo:lo + per], dl[lo:lo + per]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream, split_small=SPLIT)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    lat = np.array(lat[20:]) * 1e6
+    return {"spans_per_batch": int(min(per, n)), "p50_us": round(float(np.percentile(lat, 50)), 1),
+            "p99_us": round(float(np.percentile(lat, 99)), 1)}
+
+
 def run_mixed(eng, d, stream, rng, gib):
     nbytes = int(gib * 2**30)
     host = rng.integers(0, 256, nbytes, dtype=np.uint8)
     dbuf = torch.from_numpy(host).to(d)
-    res = {"config": "3 mixed (Zipf 0.99, SST-packed, unaligned)", "buckets": {}}
+    res = {"config": "3 mixed (Zipf 0.99, SST-packed, unaligned)", "split_small": SPLIT,
+           "buckets": {}}
     offs, lens, L = zipf_spans(rng, nbytes, BUCKETS)
     do, dl = dev(offs, d), dev(lens, d)
     out = torch.empty(offs.size, dtype=torch.int32, device=d)
@@ -89,7 +111,8 @@ def run_mixed(eng, d, stream, rng, gib):
     got = out.cpu().numpy().view(np.uint32)
     res["mixed"] = {"spans": int(offs.size), "bytes": int(lens.sum()),
                     "GiBps": round(float(lens.sum()) / t / 2**30, 1),
-                    "mismatches_in_sample": check_sample(host, offs, lens, got, rng)}
+                    "mismatches_in_sample": check_sample(host, offs, lens, got, rng),
+                    "sst_batch_latency": batch_latency(eng, dbuf, do, dl, stream)}
     for b in BUCKETS:  # one batch per bucket: same packing, only this size
         ob, lb, _ = zipf_spans(rng, nbytes, [b])
         dob, dlb = dev(ob, d), dev(lb, d)
@@ -101,23 +124,9 @@ def run_mixed(eng, d, stream, rng, gib):
         res["buckets"][str(b)] = {"spans": int(ob.size),
                                   "GiBps": round(float(lb.sum()) / tb / 2**30, 1),
                                   "mismatches_in_sample": check_sample(host, ob, lb, gotb, rng,
-                                                                       1000)}
-    # latency of SST-sized batches: ~2 MiB of the mixed spans per launch
-    cum = np.cumsum(lens.astype(np.int64) + 5)
-    per = int(np.searchsorted(cum, 2 << 20))
-    lat = []
-    outs = torch.empty(per, dtype=torch.int32, device=d)
-    for i in range(300):
-        lo = (i * per) % max(1, offs.size - per)
-        o_i, l_i = do[lo:lo + per], dl[lo:lo + per]
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream, split_small=SPLIT)
-        torch.cuda.synchronize()
-        lat.append(time.perf_counter() - t0)
-    lat = np.array(lat[20:]) * 1e6
-    res["sst_batch_latency_us"] = {"spans_per_batch": per, "p50": round(float(np.percentile(lat, 50)), 1),
-                                   "p99": round(float(np.percentile(lat, 99)), 1)}
+                                                                       1000),
+                                  "batch_latency": batch_latency(eng, dbuf, dob, dlb, stream,
+                                                                 reps=100)}
     del dbuf
     return res
 

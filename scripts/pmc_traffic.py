@@ -25,7 +25,7 @@ def per_kernel(d, counter, kernel_sub):
 
 def main():
     fdir, wdir, key, prefix = sys.argv[1:5]
-    kern = "crc32c_spans_kernel" if key.startswith("spans") else "crc32c_strided_kernel"
+    kern = "crc32c_lds_spans_kernel" if key.startswith("spans") else "crc32c_lds_strided_kernel"
     f = per_kernel(fdir, "FETCH_SIZE", kern)
     w = per_kernel(wdir, "WRITE_SIZE", kern)
     if not f or not w:

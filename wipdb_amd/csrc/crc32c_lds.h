@@ -13,7 +13,11 @@
 //                   replica r (0..7) at 32t + 4r = T[3 - t][b] (the table of
 //                   byte position t of a word);
 //                   bytes [128, 256): fold level-1 tables, entry (a, p) at
-//                   128 + (4a + p) * 4 = shift(b << 8p, 64a bytes), a = 1..7.
+//                   128 + (4a + p) * 4 = shift(b << 8p, 64a bytes), a = 1..7;
+//                   the a = 0 column (bytes 128..143, an identity shift
+//                   nobody looks up) of rows 16w .. 16w + 15 holds wave w's
+//                   16-byte aux pieces: the tail chunks and trailer chunks
+//                   of its segments, DMA'd in with the segment.
 //   [96, 160 KiB)   16 wave slots of 4 KiB: the segment being DMA'd in.
 //
 // Bank rule (ds_read_b32: lanes 0-31 and 32-63 are serviced separately,
@@ -48,6 +52,13 @@ constexpr uint32_t kLdsBytes = kLdsSlots + kWaves * kSlotBytes;  // 160 KiB
 constexpr uint32_t kImageBytes = kLdsSlots;                    // tables + misc
 constexpr uint32_t kSegChunks = 256;                           // 16-B chunks per segment
 
+// aux piece k (< 16) of wave w: 16 bytes in the a = 0 column of main row 16w + k
+WIPDB_LK_HD constexpr uint32_t AuxAddr(uint32_t w, uint32_t k) {
+  return kLdsMain + (16u * w + k) * 256u + 128u;
+}
+constexpr uint32_t kAuxTail = 0;   // + g: group g's tail chunk
+constexpr uint32_t kAuxNext = 4;   // + g: the chunk after it (verify trailers)
+
 // misc word i (i < 1024) lives in the c = 0 column of level-2 row i / 4
 WIPDB_LK_HD constexpr uint32_t MiscAddr(uint32_t i) {
   return (i >> 2) * 128u + (i & 3u) * 4u;
@@ -71,17 +82,21 @@ constexpr uint32_t kFlagMask = 0x2;
 constexpr uint32_t kClass4Chunks = 64;
 constexpr uint32_t kClass2Chunks = 128;
 constexpr uint32_t kListCut = 0x80000000u;   // id word: class-1 entry stops after its first segment
-constexpr uint32_t kListCont = 0x40000000u;  // id word: continues from the partial CRC of span id
-constexpr uint32_t kListIdMask = 0x3fffffffu;
-constexpr uint64_t kMaxListSpans = uint64_t(1) << 30;
+constexpr uint32_t kListIdMask = 0x7fffffffu;
+constexpr uint32_t kLinkClass4 = 0x80000000u;  // link word: the remainder is in the class-4 list
+constexpr uint64_t kMaxListSpans = uint64_t(1) << 30;  // link positions are 30 bits
 
 // One size-class list (struct of arrays, device memory); `count` is a device
-// counter the partition kernel fills.
+// counter the partition kernel fills.  A cut class-1 entry's `link` names its
+// remainder's entry (kLinkClass4 | position); the class-1 kernel writes the
+// partial CRC into that entry's init column, which the class-2/4 kernel
+// (launched after it) then continues from.
 struct SpanList {
   uint64_t* off;   // byte offset of the (remainder's) first byte from the batch base
   uint32_t* len;   // bytes (verify: including the type byte)
-  uint32_t* init;  // init_crc (continuations: unused)
-  uint32_t* id;    // output slot | kListCut | kListCont
+  uint32_t* init;  // init_crc (remainders: the partial CRC, written by the class-1 kernel)
+  uint32_t* id;    // output slot | kListCut
+  uint32_t* link;  // class 1, cut: the remainder's list entry
   uint32_t* count;
 };
 

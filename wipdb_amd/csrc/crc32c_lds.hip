@@ -36,9 +36,11 @@
 //     first word (the register is 0 there), so it equals ~init at the first
 //     real byte.  Later segments of a span carry the register on.  Any
 //     offset / length / init is bit-exact.
-// Descriptors, tail chunks and stored trailers are scalar (SMEM) loads;
-// every vector-memory instruction is a DMA or a result store, counted by
-// hand (s_waitcnt vmcnt) -- see issue order in run().
+// Descriptors are scalar (SMEM) loads issued an iteration ahead; a span's
+// tail chunk and stored trailer come in with its segment as one-lane DMAs
+// into per-wave aux pieces.  Every vector-memory instruction is a DMA or a
+// result store, counted by hand (s_waitcnt vmcnt) -- see the issue order in
+// run1().
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -308,39 +310,6 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
 }
 
-// Scalar (SMEM) loads of a uniform address, waited for in the same asm
-// statement.  The data pointers of a batch are not kernel arguments the
-// compiler can prove unclobbered, so plain C++ would emit vector loads --
-// which would break the hand-counted vmcnt pipeline above.
-__device__ __forceinline__ u32x4 sload4(uint64_t a) {
-  u32x4 v;
-  asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
-  return v;
-}
-__device__ __forceinline__ uint64_t sload2(uint64_t a) {
-  uint64_t v;
-  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
-  return v;
-}
-__device__ __forceinline__ uint32_t sload1(uint64_t a) {
-  uint32_t v;
-  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
-  return v;
-}
-// LE32 at byte sh / 8 of the 8 bytes v
-__device__ __forceinline__ uint32_t funnel(uint64_t v, uint32_t sh) {
-  return static_cast<uint32_t>(v >> sh);
-}
-
-// LE32 at any address (ReadBlock's trailer, kv/src/table/format.cc:91-93):
-// the second dword only when the value straddles it, so nothing past the
-// 8-byte block holding its last byte is read.
-__device__ __forceinline__ uint32_t load_le32(uint64_t a) {
-  const uint32_t sh = static_cast<uint32_t>(a & 3u) * 8u;
-  const uint64_t al = a & ~uint64_t(3);
-  return sh ? funnel(sload2(al), sh) : sload1(al);
-}
-
 // The table image (tables + misc words) into LDS [0, 96 KiB): wave w copies
 // 6 KiB with 6 DMAs.  Ends with the workgroup barrier.
 __device__ __forceinline__ void load_image(const uint8_t* image, uint32_t w, uint32_t l) {
@@ -354,18 +323,18 @@ __device__ __forceinline__ void load_image(const uint8_t* image, uint32_t w, uin
 
 // ---------------------------------------------------------------------------
 // Span sources (all values uniform).  Addresses are byte offsets from the
-// source's base pointer.
+// source's base pointer.  Descriptor columns are const __restrict__ kernel
+// arguments, so the compiler loads them with SMEM (asynchronously, waited
+// for at first use).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSpanCut = 1u;   // G = 1 list entry: stop after the first segment
-constexpr uint32_t kSpanCont = 2u;  // G > 1 list entry: continue from the partial CRC
-
 struct SpanD {
   uint64_t a;      // offset of the first byte from the source base
   uint32_t n;      // bytes
   uint32_t init;   // Extend's init_crc
-  uint32_t flags;  // kSpanCut / kSpanCont
+  uint32_t link;   // class-1 list entry cut after its first segment: kLinkValid | remainder
   uint64_t id;     // output slot
 };
+constexpr uint32_t kLinkValid = 0x40000000u;  // SpanD.link: the span is cut (link in low bits)
 
 // Descriptor batch: span i = base + offsets[i], lengths[i] (+ extra) bytes.
 struct DescSrc {
@@ -376,13 +345,7 @@ struct DescSrc {
   uint64_t count;
   uint32_t extra;  // verify: +1 type byte
   __device__ __forceinline__ SpanD get(uint64_t s) const {
-    SpanD d;
-    d.a = off[s];
-    d.n = len[s] + extra;
-    d.init = init ? init[s] : 0u;
-    d.flags = 0u;
-    d.id = s;
-    return d;
+    return SpanD{off[s], len[s] + extra, init ? init[s] : 0u, 0u, s};
   }
 };
 
@@ -397,24 +360,19 @@ struct StridedSrc {
   }
 };
 
-// A size-class list written by crc32c_lds_partition_kernel (SpanList,
-// crc32c_lds.h); its count is read from device memory at kernel start.
+// A size-class list written by crc32c_lds_partition_kernel (SpanList).
 struct ListSrc {
   const uint8_t* base;
   const uint64_t* off;
   const uint32_t* len;
   const uint32_t* init;
   const uint32_t* id;
+  const uint32_t* link;
   uint64_t count;
-  // scalar loads (the list arrays are written by the partition kernel, so
-  // the compiler cannot prove them read-only: plain loads would be vector)
   __device__ __forceinline__ SpanD get(uint64_t s) const {
-    const uint32_t w = sload1(reinterpret_cast<uint64_t>(id + s));
-    return SpanD{sload2(reinterpret_cast<uint64_t>(off + s)),
-                 sload1(reinterpret_cast<uint64_t>(len + s)),
-                 sload1(reinterpret_cast<uint64_t>(init + s)),
-                 ((w & kListCut) ? kSpanCut : 0u) | ((w & kListCont) ? kSpanCont : 0u),
-                 w & kListIdMask};
+    const uint32_t w = id[s];
+    const uint32_t lk = (w & kListCut) ? (link[s] & (kLinkClass4 | 0x3fffffffu)) | kLinkValid : 0u;
+    return SpanD{off[s], len[s], init[s], lk, w & kListIdMask};
   }
 };
 
@@ -430,6 +388,7 @@ struct Seg {
   uint32_t o, e;  // last segment: tail bytes [o, e) of the chunk at a0 + 16 nc
   uint32_t flags;
   uint32_t init;  // first segment: the span's init
+  uint32_t link;  // cut: where its partial CRC goes
   uint64_t id;    // output slot
 };
 
@@ -449,7 +408,7 @@ struct Geo {
 // A span being walked segment by segment (G = 1).
 struct Walk {
   uint64_t a0, id;
-  uint32_t f, h, t, init, k, nseg;
+  uint32_t f, h, t, init, k, nseg, link;
   bool cut, valid;
 
   __device__ __forceinline__ void start(const uint8_t* base, const SpanD& d) {
@@ -460,8 +419,9 @@ struct Walk {
     a0 = d.a - h;
     init = d.init;
     id = d.id;
+    link = d.link;
     k = 0;
-    cut = (d.flags & kSpanCut) != 0u;
+    cut = (d.link & kLinkValid) != 0u;
     nseg = cut ? 1u : (f == 0u ? 1u : (f + kSegChunks - 1u) / kSegChunks);
     valid = true;
   }
@@ -478,6 +438,7 @@ struct Walk {
     g.e = (last && !cut) ? t : 0u;
     g.flags = kSegValid | (k == 0u ? kSegFirst : 0u) | (last ? kSegLast : 0u) | (cut ? kSegCut : 0u);
     g.init = init;
+    g.link = link;
     g.id = id;
     if (last) valid = false;
     ++k;
@@ -496,6 +457,21 @@ __device__ __forceinline__ uint32_t head_mask(uint32_t h, uint32_t ww) {
   return h >= 4u * ww + 4u ? 0u : (h <= 4u * ww ? ~0u : (~0u << (8u * (h - 4u * ww))));
 }
 
+// LE32 at byte e (< 16) of the 32 bytes lo || hi (a verify trailer).
+__device__ __forceinline__ uint32_t le32_at(const u32x4& lo, const u32x4& hi, uint32_t e) {
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint32_t a = w[0], b = w[1];
+#pragma unroll
+  for (uint32_t i = 1; i < 4; ++i) {
+    if ((e >> 2) == i) {
+      a = w[i];
+      b = w[i + 1];
+    }
+  }
+  const uint32_t sh = (e & 3u) * 8u;
+  return sh ? (a >> sh) | (b << (32u - sh)) : a;
+}
+
 // ---------------------------------------------------------------------------
 // Per-workgroup unit counter: unit u of workgroup wg is span
 // ((u / 16) * grid + wg) * 16 + u % 16 -- blocks of 16 spans round robin
@@ -511,12 +487,19 @@ __device__ __forceinline__ uint64_t grab_units(uint32_t l) {
   return (static_cast<uint64_t>(u >> 4) * gridDim.x + blockIdx.x) * 16u + (u & 15u);
 }
 
+// One lane's DMA of a 16-byte chunk at base + off into an aux piece (the
+// instruction runs with lane 0 alone: LDS destination M0 + 16 * 0).
+__device__ __forceinline__ void dma_piece(uint32_t l, uint64_t base, uint32_t off, uint32_t dst) {
+  if (l == 0u) dma1nt(base, dst, off);
+}
+
 // Lane-invariant pieces of the pipeline.
 struct Pipe {
-  uint32_t l, slot, cm;
+  uint32_t l, w, slot, cm;
   uint32_t rpos[4];
   __device__ __forceinline__ void init(uint32_t lane, uint32_t wave) {
     l = lane;
+    w = wave;
     slot = kLdsSlots + wave * kSlotBytes;
     // DMA load q, lane m: chunk 64q + cm of the 256-chunk window
     cm = 4u * (lane >> 2) + (((lane & 3u) - (lane >> 4)) & 3u);
@@ -534,11 +517,18 @@ struct Pipe {
       W[4 * i + 2] = d.z;
       W[4 * i + 3] = d.w;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is free again
   }
-  // DMA window instructions [q0, q0 + nq) of a window of `cap` chunks whose
-  // last nc hold a segment at base: chunks in front of it re-read its first
-  // chunk (zeroed later).
+  __device__ __forceinline__ u32x4 piece(uint32_t k) const {
+    return *reinterpret_cast<l_u32x4*>(static_cast<uintptr_t>(AuxAddr(w, k)));
+  }
+  // Every LDS read of the slot and the pieces has returned: the next DMA may
+  // overwrite them.
+  __device__ __forceinline__ void release() const {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // DMA window loads [q0, q0 + NQ) of a window of `cap` chunks whose last
+  // nc hold a segment at base: chunks in front of it re-read its first chunk
+  // (zeroed later).
   template <uint32_t NQ>
   __device__ __forceinline__ void issue(uint64_t base, uint32_t q0, uint32_t cap, uint32_t nc) const {
     // window chunk 64 j + cm of the group (load q0 + j) is segment chunk
@@ -547,13 +537,24 @@ struct Pipe {
     const uint32_t o0 = static_cast<uint32_t>(max(b, 0));
     const uint32_t o1 = static_cast<uint32_t>(max(b + 1024, 0));
     if constexpr (NQ == 4) {
-      dma4(base, slot, o0, o1, static_cast<uint32_t>(max(b + 2048, 0)),
-           static_cast<uint32_t>(max(b + 3072, 0)));
+      if (nc == cap)
+        dma4(base, slot, 16u * cm, 16u * cm + 1024u, 16u * cm + 2048u, 16u * cm + 3072u);
+      else
+        dma4(base, slot, o0, o1, static_cast<uint32_t>(max(b + 2048, 0)),
+             static_cast<uint32_t>(max(b + 3072, 0)));
     } else if constexpr (NQ == 2) {
       dma2(base, slot + 1024u * q0, o0, o1);
     } else {
       dma1nt(base, slot + 1024u * q0, o0);
     }
+  }
+  // A span's end chunks into aux pieces kAuxTail + g (its tail chunk) and
+  // kAuxNext + g (the chunk after it, when a verify trailer at byte e
+  // straddles the two).  tail: a ragged tail exists; trailer: verify.
+  __device__ __forceinline__ void issue_end(uint64_t end_chunk, uint32_t g, bool tail, bool trailer,
+                                            uint32_t e) const {
+    if (tail || trailer) dma_piece(l, end_chunk, 0u, AuxAddr(w, kAuxTail + g));
+    if (trailer && e > 12u) dma_piece(l, end_chunk, 16u, AuxAddr(w, kAuxNext + g));
   }
 };
 
@@ -562,11 +563,13 @@ struct Pipe {
 // of vector-memory instructions per wave:
 //   DMA(seg i) ... result store(seg i-1) ... DMA(seg i+1) ...
 // so waiting for seg i's DMA is vmcnt(1) when a store followed it, else 0.
-// OUT: 0 = CRC (masked with kFlagMask), 1 = verify status byte.
+// OUT: 0 = CRC (masked with kFlagMask), 1 = verify status byte.  A cut span
+// (class-1 list entry) writes its unmasked partial CRC into the init column
+// of its remainder's class-2 / class-4 list entry (rem2 / rem4).
 // ---------------------------------------------------------------------------
 template <int OUT, typename Src>
-__device__ __forceinline__ void run1(const Src& src, void* out, uint32_t* partial, uint32_t flags,
-                                     const uint8_t* image) {
+__device__ __forceinline__ void run1(const Src& src, void* out, uint32_t flags, uint32_t* rem2,
+                                     uint32_t* rem4, const uint8_t* image) {
   const uint32_t l = threadIdx.x & 63u;
   const uint32_t w = uni(threadIdx.x >> 6);
   const uint64_t count = src.count;
@@ -578,44 +581,31 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t* partia
   const bool msk = (flags & kFlagMask) != 0u;
   const uint64_t sbase = reinterpret_cast<uint64_t>(src.base);
 
-  auto next_span = [&](Walk& wk) {
+  // the prefetched next span: its descriptor loads are issued an iteration
+  // before it is used, so their latency hides behind a segment
+  struct Pref {
+    SpanD d;
+    bool valid;
+  };
+  auto prefetch = [&](Pref& p) {
     const uint64_t s = grab_units<1>(l);
-    if (s >= count) {
-      wk.valid = false;
-      return;
-    }
-    wk.start(src.base, src.get(s));
+    p.valid = s < count;
+    if (p.valid) p.d = src.get(s);
   };
   auto issue = [&](const Seg& g) {
-    if (g.nc == kSegChunks) {
-      dma4(sbase + g.a0, pp.slot, 16u * pp.cm, 16u * pp.cm + 1024u, 16u * pp.cm + 2048u,
-           16u * pp.cm + 3072u);
-    } else if (g.nc != 0u) {
-      pp.issue<4>(sbase + g.a0, 0u, kSegChunks, g.nc);
-    }
-  };
-  // scalar loads for the segment's end: its tail chunk and (verify) the
-  // stored trailer, LE32 right after the span.  Synchronous (s_load + wait
-  // in one asm statement): they are issued at the end of an iteration, when
-  // the wave is about to wait for its next DMA anyway.
-  auto load_end = [&](const Seg& g, u32x4& tail, uint32_t& stored) {
-    tail = u32x4{0, 0, 0, 0};
-    stored = 0;
-    if (!(g.flags & kSegLast)) return;
-    if (g.e != 0u) tail = sload4(sbase + g.a0 + 16u * g.nc);
-    if (OUT == 1 && !(g.flags & kSegCut)) stored = load_le32(sbase + g.a0 + 16u * g.nc + g.e);
+    if (g.nc != 0u) pp.issue<4>(sbase + g.a0, 0u, kSegChunks, g.nc);
+    if (g.flags & kSegLast)
+      pp.issue_end(sbase + g.a0 + 16u * g.nc, 0u, g.e > g.o, OUT == 1 && !(g.flags & kSegCut), g.e);
   };
 
-  Walk wk, pf;
-  wk.valid = pf.valid = false;
-  next_span(wk);
-  if (!wk.valid) return;
-  next_span(pf);
+  Walk wk;
+  Pref pf;
+  prefetch(pf);
+  if (!pf.valid) return;
+  wk.start(src.base, pf.d);
+  prefetch(pf);
   Seg cur = wk.next();
   issue(cur);
-  u32x4 tail;
-  uint32_t stored;
-  load_end(cur, tail, stored);
   uint32_t chain = 0;  // register carried between the segments of a span
   bool stored_prev = false;
 
@@ -624,6 +614,12 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t* partia
     else wait_vm<0>();
     uint32_t W[16];
     pp.read(W);
+    u32x4 tail{0, 0, 0, 0}, next{0, 0, 0, 0};
+    if (cur.flags & kSegLast) {
+      tail = pp.piece(kAuxTail);
+      if (OUT == 1 && cur.e > 12u) next = pp.piece(kAuxNext);
+    }
+    pp.release();
     // the next segment: the rest of this span, or the prefetched span
     Seg nxt;
     nxt.flags = 0;
@@ -631,7 +627,7 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t* partia
     if (wk.valid) {
       nxt = wk.next();
     } else if (pf.valid) {
-      wk = pf;
+      wk.start(src.base, pf.d);
       took_pf = true;
       nxt = wk.next();
     }
@@ -664,15 +660,17 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t* partia
 
     bool did_store = false;
     if (cur.flags & kSegLast) {
+      tail = u32x4{uni(tail.x), uni(tail.y), uni(tail.z), uni(tail.w)};
       if (cur.e > cur.o) R = feed_tail(lk, l, R, tail, cur.o, cur.e);
       const uint32_t crc = ~R;
       did_store = true;
       if (l == 0u) {
         if (cur.flags & kSegCut) {
-          // partial CRC of a span a size-class kernel finishes
-          if (OUT == 1) partial[cur.id] = crc;
-          else static_cast<uint32_t*>(out)[cur.id] = crc;
+          // the partial CRC continues in the remainder's list entry
+          uint32_t* dst = (cur.link & kLinkClass4) ? rem4 : rem2;
+          dst[cur.link & 0x3fffffffu] = crc;
         } else if (OUT == 1) {
+          const uint32_t stored = le32_at(tail, next, cur.e);
           static_cast<uint8_t*>(out)[cur.id] = unmask_crc(stored) == crc ? 1u : 0u;
         } else {
           static_cast<uint32_t*>(out)[cur.id] = msk ? mask_crc(crc) : crc;
@@ -684,9 +682,7 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t* partia
     stored_prev = did_store;
 
     if (!(nxt.flags & kSegValid)) break;
-    // refill the span prefetch and the next segment's scalar loads
-    if (took_pf) next_span(pf);
-    load_end(nxt, tail, stored);
+    if (took_pf) prefetch(pf);
     cur = nxt;
   }
 }
@@ -697,18 +693,17 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t* partia
 // ---------------------------------------------------------------------------
 template <int G>
 struct GroupSpan {
-  uint64_t a0;      // offset of the span's first chunk
-  uint32_t nc;      // full chunks (<= 256 / G)
-  uint32_t h, o, e; // head bytes, tail range
-  uint32_t inj;     // register entering the first chunk
-  uint32_t init;    // ~register for nc == 0 (all-tail spans)
+  uint64_t a0;       // offset of the span's first chunk
+  uint32_t nc;       // full chunks (<= 256 / G)
+  uint32_t h, o, e;  // head bytes, tail range
+  uint32_t init;
   uint32_t id;
-  bool valid, cont;
+  bool valid;
 };
 
 template <int G, int OUT>
-__device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t* partial,
-                                      uint32_t flags, const uint8_t* image) {
+__device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t flags,
+                                      const uint8_t* image) {
   constexpr uint32_t LG = 64u / G, CAP = kSegChunks / G;
   const uint32_t l = threadIdx.x & 63u;
   const uint32_t w = uni(threadIdx.x >> 6);
@@ -721,51 +716,49 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t* p
   const bool msk = (flags & kFlagMask) != 0u;
   const uint64_t sbase = reinterpret_cast<uint64_t>(src.base);
   const uint32_t gl = l % LG;
-  const uint32_t* cont_src = OUT == 1 ? partial : static_cast<const uint32_t*>(out);
 
   typedef GroupSpan<G> GS;
-  auto load = [&](GS (&gs)[G]) {
+  // descriptors of the next G units (SMEM, waited for at first use)
+  struct Pref {
+    SpanD d[G];
+    bool valid[G];
+  };
+  auto prefetch = [&](Pref& p) {
     const uint64_t s0 = grab_units<G>(l);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const uint64_t s = s0 + g;
-      gs[g].valid = s < count;
-      gs[g].nc = 0;
-      gs[g].h = gs[g].o = gs[g].e = 0;
-      gs[g].inj = gs[g].init = 0;
-      gs[g].id = 0;
+      p.valid[g] = s0 + g < count;
+      if (p.valid[g]) p.d[g] = src.get(s0 + g);
+    }
+  };
+  auto take = [&](const Pref& p, GS (&gs)[G]) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      gs[g].valid = p.valid[g];
+      gs[g].nc = gs[g].h = gs[g].o = gs[g].e = gs[g].init = gs[g].id = 0;
       gs[g].a0 = 0;
-      gs[g].cont = false;
-      if (!gs[g].valid) continue;
-      const SpanD d = src.get(s);
+      if (!p.valid[g]) continue;
+      const SpanD& d = p.d[g];
       const Geo geo(sbase + d.a, d.n);
       gs[g].a0 = d.a - geo.h;
       gs[g].nc = geo.f;
       gs[g].h = geo.h;
       gs[g].o = geo.f == 0u ? geo.h : 0u;
       gs[g].e = geo.t;
+      gs[g].init = d.init;
       gs[g].id = static_cast<uint32_t>(d.id);
-      gs[g].cont = (d.flags & kSpanCont) != 0u;
-      // a continuation starts 16-aligned (h = 0) from the partial CRC
-      gs[g].init = gs[g].cont ? sload1(reinterpret_cast<uint64_t>(cont_src + d.id)) : d.init;
     }
   };
   auto issue = [&](const GS (&gs)[G]) {
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-      if (gs[g].valid && gs[g].nc != 0u) {
+    for (int g = 0; g < G; ++g) {
+      if (!gs[g].valid) continue;
+      if (gs[g].nc != 0u) {
         if constexpr (G == 2) pp.issue<2>(sbase + gs[g].a0, 2u * g, CAP, gs[g].nc);
         else pp.issue<1>(sbase + gs[g].a0, static_cast<uint32_t>(g), CAP, gs[g].nc);
       }
-  };
-  auto load_end = [&](const GS (&gs)[G], u32x4 (&tail)[G], uint32_t (&stored)[G]) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      tail[g] = u32x4{0, 0, 0, 0};
-      stored[g] = 0;
-      if (!gs[g].valid) continue;
-      if (gs[g].e != 0u) tail[g] = sload4(sbase + gs[g].a0 + 16u * gs[g].nc);
-      if (OUT == 1) stored[g] = load_le32(sbase + gs[g].a0 + 16u * gs[g].nc + gs[g].e);
+      pp.issue_end(sbase + gs[g].a0 + 16u * gs[g].nc, static_cast<uint32_t>(g),
+                   gs[g].e > gs[g].o, OUT == 1, gs[g].e);
     }
   };
   // per-lane value of this lane's group: masked selects on per-group lane
@@ -784,14 +777,13 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t* p
     return r;
   };
 
+  Pref pf;
   GS cur[G], nxt[G];
-  load(cur);
-  if (!cur[0].valid) return;
+  prefetch(pf);
+  if (!pf.valid[0]) return;
+  take(pf, cur);
+  prefetch(pf);
   issue(cur);
-  u32x4 tail[G];
-  uint32_t stored[G];
-  load_end(cur, tail, stored);
-  load(nxt);
   bool stored_prev = false;
 
   for (;;) {
@@ -799,7 +791,18 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t* p
     else wait_vm<0>();
     uint32_t W[16];
     pp.read(W);
-    if (nxt[0].valid) issue(nxt);
+    u32x4 tail[G], next[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      tail[g] = pp.piece(kAuxTail + g);
+      next[g] = OUT == 1 ? pp.piece(kAuxNext + g) : u32x4{0, 0, 0, 0};
+    }
+    pp.release();
+    const bool more = pf.valid[0];
+    if (more) {
+      take(pf, nxt);
+      issue(nxt);
+    }
 
     // ---- the G spans of this iteration ----
     uint32_t inj_g[G], nc_g[G], h_g[G];
@@ -828,8 +831,7 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t* p
     }
     const auto Rg = fold<G>(lk, l, scan(lk, W));
     // registers after the main chunks; all-tail spans start from ~init
-    uint32_t R[G], o_g[G], e_g[G];
-    uint32_t tw[4][G];
+    uint32_t R[G], o_g[G], e_g[G], tw[4][G], nw[4][G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       R[g] = cur[g].nc == 0u ? ~cur[g].init : Rg[g];
@@ -839,44 +841,46 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t* p
       tw[1][g] = tail[g].y;
       tw[2][g] = tail[g].z;
       tw[3][g] = tail[g].w;
+      nw[0][g] = next[g].x;
+      nw[1][g] = next[g].y;
+      nw[2][g] = next[g].z;
+      nw[3][g] = next[g].w;
     }
-    // tails, all groups in the same instructions (lane l serves its group)
+    // tails, all groups in the same instructions (lane l serves its group;
+    // the aux pieces were read by every lane, so the words are uniform per
+    // group already)
     uint32_t r = pick(R);
+    const uint32_t o = pick(o_g), e = pick(e_g);
+    const u32x4 t{pick(tw[0]), pick(tw[1]), pick(tw[2]), pick(tw[3])};
     {
       uint32_t need = 0;
 #pragma unroll
       for (int g = 0; g < G; ++g) need |= e_g[g];
-      if (need != 0u) {
-        const uint32_t o = pick(o_g), e = pick(e_g);
-        const u32x4 t{pick(tw[0]), pick(tw[1]), pick(tw[2]), pick(tw[3])};
-        r = feed_tail_lanes(lk, l, r, t, o, e);
-      }
+      if (need != 0u) r = feed_tail_lanes(lk, l, r, t, o, e);
     }
-    // results: the group leaders store
     const uint32_t val = ~r;
     bool valid_l = false;
-    uint32_t ids[G], st[G];
+    uint32_t ids[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       ids[g] = cur[g].id;
-      st[g] = stored[g];
       valid_l = valid_l || (gm[g] != 0u && cur[g].valid);
     }
     const uint32_t myid = pick(ids);
     if (gl == 0u && valid_l) {
       if (OUT == 1) {
-        static_cast<uint8_t*>(out)[myid] = unmask_crc(pick(st)) == val ? 1u : 0u;
+        const u32x4 nx{pick(nw[0]), pick(nw[1]), pick(nw[2]), pick(nw[3])};
+        static_cast<uint8_t*>(out)[myid] = unmask_crc(le32_at(t, nx, e)) == val ? 1u : 0u;
       } else {
         static_cast<uint32_t*>(out)[myid] = msk ? mask_crc(val) : val;
       }
     }
     stored_prev = true;
 
-    if (!nxt[0].valid) break;
+    if (!more) break;
 #pragma unroll
     for (int g = 0; g < G; ++g) cur[g] = nxt[g];
-    load_end(cur, tail, stored);
-    load(nxt);
+    prefetch(pf);
   }
 }
 
@@ -889,7 +893,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const DescSrc src{base, offsets, lengths, inits, count, 0u};
-  run1<0>(src, out, nullptr, flags, image);
+  run1<0>(src, out, flags, nullptr, nullptr, image);
 }
 
 // Fixed-size blocks at a fixed stride.
@@ -897,7 +901,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t length, uint32_t init,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const StridedSrc src{base, stride, length, init, count};
-  run1<0>(src, out, nullptr, flags & kFlagMask, image);
+  run1<0>(src, out, flags & kFlagMask, nullptr, nullptr, image);
 }
 
 // Read-side verify (ReadBlock, kv/src/table/format.cc:91-99): block i =
@@ -908,49 +912,51 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
     const uint8_t* __restrict__ image) {
   const DescSrc src{base, offsets, lengths, nullptr, count, 1u};
-  run1<1>(src, status, nullptr, 0u, image);
+  run1<1>(src, status, 0u, nullptr, nullptr, image);
 }
 
-// A size-class list (HCRC_SPLIT_SMALL): G = 1 takes spans of more than
-// 2 KiB (cut ones write their partial CRC), G = 2 / 4 the spans and
-// remainders of at most 2 KiB / 1 KiB.  OUT: 0 = CRCs into out (u32), 1 =
-// verify statuses into out (u8) with the cut blocks' partials in partial.
+// A size-class list (HCRC_SPLIT_SMALL): G = 1 takes the spans of more than
+// 128 chunks (cut ones write their partial CRC into rem2 / rem4, the init
+// columns of the class-2 / class-4 lists), G = 2 / 4 the spans and
+// remainders of at most 128 / 64 chunks.  OUT: 0 = CRCs into out (u32),
+// 1 = verify statuses into out (u8).
 template <int G, int OUT>
 __global__ __launch_bounds__(kThreads) void crc32c_lds_list_kernel(
-    const uint8_t* __restrict__ base, SpanList list, void* out, uint32_t* partial, uint32_t flags,
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ init,
+    const uint32_t* __restrict__ id, const uint32_t* __restrict__ link,
+    const uint32_t* __restrict__ count, void* out, uint32_t* rem2, uint32_t* rem4, uint32_t flags,
     const uint8_t* __restrict__ image) {
-  const uint32_t n = sload1(reinterpret_cast<uint64_t>(list.count));
-  const ListSrc src{base, list.off, list.len, list.init, list.id, n};
-  if constexpr (G == 1) run1<OUT>(src, out, partial, flags, image);
-  else run_g<G, OUT>(src, out, partial, flags, image);
+  const ListSrc src{base, off, len, init, id, link, *count};
+  if constexpr (G == 1) run1<OUT>(src, out, flags, rem2, rem4, image);
+  else run_g<G, OUT>(src, out, flags, image);
 }
-template __global__ void crc32c_lds_list_kernel<1, 0>(const uint8_t*, SpanList, void*, uint32_t*,
-                                                      uint32_t, const uint8_t*);
-template __global__ void crc32c_lds_list_kernel<2, 0>(const uint8_t*, SpanList, void*, uint32_t*,
-                                                      uint32_t, const uint8_t*);
-template __global__ void crc32c_lds_list_kernel<4, 0>(const uint8_t*, SpanList, void*, uint32_t*,
-                                                      uint32_t, const uint8_t*);
-template __global__ void crc32c_lds_list_kernel<1, 1>(const uint8_t*, SpanList, void*, uint32_t*,
-                                                      uint32_t, const uint8_t*);
-template __global__ void crc32c_lds_list_kernel<2, 1>(const uint8_t*, SpanList, void*, uint32_t*,
-                                                      uint32_t, const uint8_t*);
-template __global__ void crc32c_lds_list_kernel<4, 1>(const uint8_t*, SpanList, void*, uint32_t*,
-                                                      uint32_t, const uint8_t*);
+#define WIPDB_LIST_KERNEL(G, OUT)                                                              \
+  template __global__ void crc32c_lds_list_kernel<G, OUT>(                                     \
+      const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, const uint32_t*,     \
+      const uint32_t*, const uint32_t*, void*, uint32_t*, uint32_t*, uint32_t, const uint8_t*)
+WIPDB_LIST_KERNEL(1, 0);
+WIPDB_LIST_KERNEL(2, 0);
+WIPDB_LIST_KERNEL(4, 0);
+WIPDB_LIST_KERNEL(1, 1);
+WIPDB_LIST_KERNEL(2, 1);
+WIPDB_LIST_KERNEL(4, 1);
+#undef WIPDB_LIST_KERNEL
 
 // ---------------------------------------------------------------------------
 // Partition into size-class lists (HCRC_SPLIT_SMALL).  Workgroup w scans a
 // contiguous range of the batch twice: counts per class, one global atomic
 // per class to reserve its slices, then writes the entries (wave-ordered
 // through a ballot prefix), so each list keeps the batch's memory order
-// piecewise.
+// piecewise.  A cut span's class-1 entry links to its remainder's entry.
 // ---------------------------------------------------------------------------
 constexpr int kPartThreads = 256;
 
 struct Classified {
-  uint32_t cls;      // 1, 2 or 4
-  bool cut;          // class 1: remainder entry too
-  uint32_t rcls;     // the remainder's class
-  uint64_t roff;     // remainder: offset of its first byte
+  uint32_t cls;   // 1, 2 or 4
+  bool cut;       // class 1: a remainder entry too
+  uint32_t rcls;  // the remainder's class
+  uint64_t roff;  // remainder: offset of its first byte
   uint32_t rlen;
 };
 
@@ -973,13 +979,7 @@ __device__ __forceinline__ Classified classify(const uint8_t* base, uint64_t off
   return c;
 }
 
-__device__ __forceinline__ void put(const SpanList& L, uint32_t pos, uint64_t off, uint32_t len,
-                                    uint32_t init, uint32_t id) {
-  L.off[pos] = off;
-  L.len[pos] = len;
-  L.init[pos] = init;
-  L.id[pos] = id;
-}
+__device__ __forceinline__ int class_slot(uint32_t cls) { return cls == 1u ? 0 : (cls == 2u ? 1 : 2); }
 
 __global__ __launch_bounds__(kPartThreads) void crc32c_lds_partition_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
@@ -992,29 +992,26 @@ __global__ __launch_bounds__(kPartThreads) void crc32c_lds_partition_kernel(
   const uint64_t hi = lo + per < count ? lo + per : count;
   if (tid < 3) cnt[tid] = 0;
   __syncthreads();
-  auto slot = [](uint32_t cls) { return cls == 1u ? 0u : (cls == 2u ? 1u : 2u); };
   // pass 1: count
   uint32_t mine[3] = {0, 0, 0};
   for (uint64_t s = lo + tid; s < hi; s += kPartThreads) {
     const Classified c = classify(base, offsets[s], lengths[s] + extra);
-    ++mine[slot(c.cls)];
-    if (c.cut) ++mine[slot(c.rcls)];
+    ++mine[class_slot(c.cls)];
+    if (c.cut) ++mine[class_slot(c.rcls)];
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k)
     if (mine[k]) atomicAdd(&cnt[k], mine[k]);
   __syncthreads();
   if (tid == 0) {
-    const SpanList* L[3] = {&l1, &l2, &l4};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      pos[k] = cnt[k] ? atomicAdd(L[k]->count, cnt[k]) : 0u;
-    }
+    pos[0] = cnt[0] ? atomicAdd(l1.count, cnt[0]) : 0u;
+    pos[1] = cnt[1] ? atomicAdd(l2.count, cnt[1]) : 0u;
+    pos[2] = cnt[2] ? atomicAdd(l4.count, cnt[2]) : 0u;
   }
   __syncthreads();
-  // pass 2: write, 64 spans per wave step, positions from a ballot prefix
-  const SpanList* L[3] = {&l1, &l2, &l4};
+  // pass 2: positions (ballot prefix per wave step of 64 spans), then writes
   const uint64_t wbase = lo + (tid & ~63u);
+  const uint64_t below = (uint64_t(1) << lane) - 1u;
   for (uint64_t s0 = wbase; s0 < hi; s0 += kPartThreads) {
     const uint64_t s = s0 + lane;
     const bool live = s < hi;
@@ -1027,6 +1024,7 @@ __global__ __launch_bounds__(kPartThreads) void crc32c_lds_partition_kernel(
       ini = inits ? inits[s] : 0u;
       c = classify(base, off, n);
     }
+    uint32_t pa = 0, pb = 0;  // this lane's entry positions (primary, remainder)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const uint32_t cls = k == 0 ? 1u : (k == 1 ? 2u : 4u);
@@ -1039,13 +1037,24 @@ __global__ __launch_bounds__(kPartThreads) void crc32c_lds_partition_kernel(
       uint32_t p0 = 0;
       if (lane == 0u) p0 = atomicAdd(&pos[k], na + nb);
       p0 = __builtin_amdgcn_readfirstlane(p0);
-      const uint64_t below = (uint64_t(1) << lane) - 1u;
-      if (a)
-        put(*L[k], p0 + __builtin_popcountll(ma & below), off, n, ini,
-            static_cast<uint32_t>(s) | (c.cut ? kListCut : 0u));
-      if (b)
-        put(*L[k], p0 + na + __builtin_popcountll(mb & below), c.roff, c.rlen, 0u,
-            static_cast<uint32_t>(s) | kListCont);
+      if (a) pa = p0 + __builtin_popcountll(ma & below);
+      if (b) pb = p0 + na + __builtin_popcountll(mb & below);
+    }
+    if (live) {
+      const SpanList& L = c.cls == 1u ? l1 : (c.cls == 2u ? l2 : l4);
+      L.off[pa] = off;
+      L.len[pa] = n;
+      L.init[pa] = ini;
+      L.id[pa] = static_cast<uint32_t>(s) | (c.cut ? kListCut : 0u);
+      L.link[pa] = c.cut ? (pb | (c.rcls == 4u ? kLinkClass4 : 0u)) : 0u;
+      if (c.cut) {
+        const SpanList& R = c.rcls == 2u ? l2 : l4;
+        R.off[pb] = c.roff;
+        R.len[pb] = c.rlen;
+        R.init[pb] = 0u;  // the class-1 kernel writes the partial CRC here
+        R.id[pb] = static_cast<uint32_t>(s);
+        R.link[pb] = 0u;
+      }
     }
   }
 }

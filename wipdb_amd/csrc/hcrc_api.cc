@@ -39,7 +39,9 @@ __global__ void crc32c_lds_strided_kernel(const uint8_t*, uint64_t, uint32_t, ui
 __global__ void crc32c_lds_verify_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                          uint8_t*, uint64_t, const uint8_t*);
 template <int G, int OUT>
-__global__ void crc32c_lds_list_kernel(const uint8_t*, SpanList, void*, uint32_t*, uint32_t,
+__global__ void crc32c_lds_list_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
+                                       const uint32_t*, const uint32_t*, const uint32_t*,
+                                       const uint32_t*, void*, uint32_t*, uint32_t*, uint32_t,
                                        const uint8_t*);
 __global__ void crc32c_lds_partition_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                             const uint32_t*, uint64_t, uint32_t, SpanList,
@@ -306,9 +308,8 @@ int LaunchClasses(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const
                   const uint32_t* init, void* out, size_t n, int out_kind, bool mask,
                   hipStream_t st) {
   // scratch: 3 lists of n entries -- the u64 offset columns first (8-byte
-  // aligned), then the u32 columns, the 3 counters (16 bytes), the verify
-  // partials
-  const size_t bytes = n * (3 * 8 + 3 * 12) + 16 + (out_kind ? n * 4 : 0);
+  // aligned), then the u32 columns (len, init, id, link), the 3 counters
+  const size_t bytes = n * (3 * 8 + 3 * 16) + 16;
   uint8_t* scratch = nullptr;
   HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), bytes, ctx->scratch_pool,
                                     st));
@@ -322,12 +323,11 @@ int LaunchClasses(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const
     l.len = reinterpret_cast<uint32_t*>(p);
     l.init = l.len + n;
     l.id = l.init + n;
-    p += n * 12;
+    l.link = l.id + n;
+    p += n * 16;
   }
   uint32_t* counts = reinterpret_cast<uint32_t*>(p);
-  p += 16;
   for (int k = 0; k < 3; ++k) L[k].count = counts + k;
-  uint32_t* partial = out_kind ? reinterpret_cast<uint32_t*>(p) : nullptr;
 
   int rc = hipMemsetAsync(counts, 0, 16, st) == hipSuccess ? HCRC_OK : HCRC_ERR_HIP;
   if (rc == HCRC_OK) {
@@ -339,21 +339,23 @@ int LaunchClasses(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const
   }
   const uint32_t kf = mask ? lk::kFlagMask : 0u;
   const dim3 grid(ctx->num_cu), blk(lk::kThreads);
+  // class 1 first: its cut entries write the class-2/4 remainders' inits
+  auto launch = [&](auto kernel, const lk::SpanList& l) {
+    hipLaunchKernelGGL(kernel, grid, blk, lk::kLdsBytes, st, base,
+                       static_cast<const uint64_t*>(l.off), static_cast<const uint32_t*>(l.len),
+                       static_cast<const uint32_t*>(l.init), static_cast<const uint32_t*>(l.id),
+                       static_cast<const uint32_t*>(l.link), static_cast<const uint32_t*>(l.count),
+                       out, L[1].init, L[2].init, kf, static_cast<const uint8_t*>(ctx->d_image));
+  };
   if (rc == HCRC_OK) {
     if (out_kind) {
-      hipLaunchKernelGGL((lk::crc32c_lds_list_kernel<1, 1>), grid, blk, lk::kLdsBytes, st, base,
-                         L[0], out, partial, kf, ctx->d_image);
-      hipLaunchKernelGGL((lk::crc32c_lds_list_kernel<2, 1>), grid, blk, lk::kLdsBytes, st, base,
-                         L[1], out, partial, kf, ctx->d_image);
-      hipLaunchKernelGGL((lk::crc32c_lds_list_kernel<4, 1>), grid, blk, lk::kLdsBytes, st, base,
-                         L[2], out, partial, kf, ctx->d_image);
+      launch(lk::crc32c_lds_list_kernel<1, 1>, L[0]);
+      launch(lk::crc32c_lds_list_kernel<2, 1>, L[1]);
+      launch(lk::crc32c_lds_list_kernel<4, 1>, L[2]);
     } else {
-      hipLaunchKernelGGL((lk::crc32c_lds_list_kernel<1, 0>), grid, blk, lk::kLdsBytes, st, base,
-                         L[0], out, partial, kf, ctx->d_image);
-      hipLaunchKernelGGL((lk::crc32c_lds_list_kernel<2, 0>), grid, blk, lk::kLdsBytes, st, base,
-                         L[1], out, partial, kf, ctx->d_image);
-      hipLaunchKernelGGL((lk::crc32c_lds_list_kernel<4, 0>), grid, blk, lk::kLdsBytes, st, base,
-                         L[2], out, partial, kf, ctx->d_image);
+      launch(lk::crc32c_lds_list_kernel<1, 0>, L[0]);
+      launch(lk::crc32c_lds_list_kernel<2, 0>, L[1]);
+      launch(lk::crc32c_lds_list_kernel<4, 0>, L[2]);
     }
     rc = Launched();
   }
