@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Kernel time of the descriptor batch on synthetic span shapes (1 M spans
+each unless noted): which part of a span's shape costs time -- the head
+(unaligned start), the tail (length % 16), the piece (chunks past 256).
+Prints one JSON line per shape; checks a sample against the CPU path."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from wipdb_amd import Engine, cpu_batch  # noqa: E402
+
+sys.path.insert(0, os.path.join(REPO, "scripts"))
+from bench_extra import dev, time_kernel  # noqa: E402
+
+SHAPES = [  # name, start offset in slot, length, slot stride
+    ("aligned 4096", 0, 4096, 4096),
+    ("head 3, 4093 (f 256, no tail)", 3, 4093, 4096),
+    ("aligned 4099 (tail 3)", 0, 4099, 4112),
+    ("head 3, 4096 (tail 3)", 3, 4096, 4112),
+    ("aligned 4112 (piece 1)", 0, 4112, 4112),
+    ("aligned 4208 (piece 7)", 0, 4208, 4208),
+    ("head 5, 4200 (piece 6 + tail)", 5, 4200, 4224),
+]
+
+
+def main():
+    d = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(d)
+    n = 1 << 20
+    rng = np.random.default_rng(1)
+    with Engine(0) as eng:
+        buf = torch.empty(n * 4224 + 4096, dtype=torch.uint8, device=d)
+        eng.fill_splitmix64_device(buf, 5, stream=st.cuda_stream)
+        host = None
+        for name, h, ln, stride in SHAPES:
+            offs = (np.arange(n, dtype=np.uint64) * stride + h).astype(np.uint64)
+            lens = np.full(n, ln, np.uint32)
+            do, dl = dev(offs, d), dev(lens, d)
+            out = torch.empty(n, dtype=torch.int32, device=d)
+            t = time_kernel(lambda: eng.batch_device(buf, do, dl, None, out, stream=st.cuda_stream), st, 20)
+            if host is None:
+                host = buf.cpu().numpy()
+            idx = rng.choice(n, 2000, replace=False)
+            got = out.cpu().numpy().view(np.uint32)[idx]
+            bad = int((cpu_batch(host, offs[idx], lens[idx]) != got).sum())
+            print(json.dumps({"shape": name, "ms": round(t * 1e3, 4),
+                              "GiBps": round(float(lens.sum()) / t / 2**30, 1), "mismatches": bad}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

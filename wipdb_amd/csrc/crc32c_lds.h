@@ -56,8 +56,8 @@ constexpr uint32_t kSegChunks = 256;                           // 16-B chunks pe
 WIPDB_LK_HD constexpr uint32_t AuxAddr(uint32_t w, uint32_t k) {
   return kLdsMain + (16u * w + k) * 256u + 128u;
 }
-constexpr uint32_t kAuxTail = 0;   // + g: group g's tail chunk
-constexpr uint32_t kAuxNext = 4;   // + g: the chunk after it (verify trailers)
+constexpr uint32_t kAuxTail = 0;   // + g (g < 8): group g's tail chunk
+constexpr uint32_t kAuxNext = 8;   // + g: the chunk after it (verify trailers)
 
 // misc word i (i < 1024) lives in the c = 0 column of level-2 row i / 4
 WIPDB_LK_HD constexpr uint32_t MiscAddr(uint32_t i) {

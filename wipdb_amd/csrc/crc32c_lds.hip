@@ -53,6 +53,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const uint32_t l_u32;
 typedef __attribute__((address_space(3))) uint32_t l_u32w;
 typedef __attribute__((address_space(3))) const u32x4 l_u32x4;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
 
 __device__ __forceinline__ uint32_t lds_ld(uint32_t a) {
   return *reinterpret_cast<l_u32*>(static_cast<uintptr_t>(a));
@@ -380,6 +382,11 @@ struct ListSrc {
 // Segments of a span (uniform).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegValid = 1u, kSegFirst = 2u, kSegLast = 4u, kSegCut = 8u;
+// kSegPiece: the span's last segment; its remainder (at most kPieceChunks
+// chunks + the tail) joins the wave's piece ring.  kSegBatch: not a segment
+// but a batch of up to 8 pieces (nc pieces from ring entry init).
+constexpr uint32_t kSegPiece = 16u, kSegBatch = 32u;
+constexpr uint32_t kPieceChunks = 32;
 
 struct Seg {
   uint64_t a0;    // offset of the segment's first chunk (16-byte aligned address)
@@ -389,6 +396,7 @@ struct Seg {
   uint32_t flags;
   uint32_t init;  // first segment: the span's init
   uint32_t link;  // cut: where its partial CRC goes
+  uint32_t pw;    // kSegPiece: the piece's chunks | tail bytes << 8
   uint64_t id;    // output slot
 };
 
@@ -409,9 +417,12 @@ struct Geo {
 struct Walk {
   uint64_t a0, id;
   uint32_t f, h, t, init, k, nseg, link;
-  bool cut, valid;
+  bool cut, piece, valid;
 
-  __device__ __forceinline__ void start(const uint8_t* base, const SpanD& d) {
+  // pieces: a span of more than 256 chunks whose last 1..kPieceChunks chunks
+  // (+ tail) would need a whole segment iteration leaves them to the piece
+  // ring instead
+  __device__ __forceinline__ void start(const uint8_t* base, const SpanD& d, bool pieces = false) {
     const Geo g(reinterpret_cast<uint64_t>(base) + d.a, d.n);
     h = g.h;
     f = g.f;
@@ -422,7 +433,9 @@ struct Walk {
     link = d.link;
     k = 0;
     cut = (d.link & kLinkValid) != 0u;
-    nseg = cut ? 1u : (f == 0u ? 1u : (f + kSegChunks - 1u) / kSegChunks);
+    const uint32_t r = f % kSegChunks;
+    piece = pieces && !cut && f > kSegChunks && r != 0u && r <= kPieceChunks;
+    nseg = cut ? 1u : (piece ? f / kSegChunks : (f == 0u ? 1u : (f + kSegChunks - 1u) / kSegChunks));
     valid = true;
   }
   __device__ __forceinline__ Seg next() {
@@ -435,10 +448,12 @@ struct Walk {
     // the tail: bytes [0, t) of the chunk after the last full one; a span
     // inside one chunk (f == 0) is all tail, bytes [h, t)
     g.o = f == 0u ? h : 0u;
-    g.e = (last && !cut) ? t : 0u;
-    g.flags = kSegValid | (k == 0u ? kSegFirst : 0u) | (last ? kSegLast : 0u) | (cut ? kSegCut : 0u);
+    g.e = (last && !cut && !piece) ? t : 0u;
+    g.flags = kSegValid | (k == 0u ? kSegFirst : 0u) | (last ? kSegLast : 0u) | (cut ? kSegCut : 0u) |
+              (last && piece ? kSegPiece : 0u);
     g.init = init;
     g.link = link;
+    g.pw = piece ? (f % kSegChunks) | (t << 8) : 0u;
     g.id = id;
     if (last) valid = false;
     ++k;
@@ -519,6 +534,10 @@ struct Pipe {
     }
   }
   __device__ __forceinline__ u32x4 piece(uint32_t k) const {
+    return *reinterpret_cast<l_u32x4*>(static_cast<uintptr_t>(AuxAddr(w, k)));
+  }
+  // aux piece k, k per lane
+  __device__ __forceinline__ u32x4 piece_lane(uint32_t k) const {
     return *reinterpret_cast<l_u32x4*>(static_cast<uintptr_t>(AuxAddr(w, k)));
   }
   // Every LDS read of the slot and the pieces has returned: the next DMA may
@@ -682,6 +701,225 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t flags, 
     stored_prev = did_store;
 
     if (!(nxt.flags & kSegValid)) break;
+    if (took_pf) prefetch(pf);
+    cur = nxt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The descriptor / strided / verify pipeline: G = 1 segments, plus pieces.
+// A span of more than 256 chunks whose last 1..32 chunks (+ tail) would cost
+// a whole 64-lane segment iteration (a table block: 4 KiB + its last entry +
+// the type byte) hands them, with the register after its last full segment,
+// to the wave's piece ring: entry k in lane k of five VGPRs.  Once 8 are
+// pending (or the wave runs out of segments), one iteration CRCs them all,
+// a piece per 8-lane group (a 32-chunk window each, two per DMA instruction
+// of half a wave), folded within the group (level 1 + DPP: no level 2).
+// ---------------------------------------------------------------------------
+// The fold of 8-lane groups: valid in each group's lane 8g.
+__device__ __forceinline__ uint32_t fold8(const Lane& k, uint32_t l, uint32_t r) {
+  uint32_t v = fold_l1(k, l, r);
+  v ^= dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v ^= dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v ^= dpp<0x104>(v);  // row_shl:4 -> lanes 8k hold their block of 8
+  return v;
+}
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t lane) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(lane << 2),
+                                                            static_cast<int>(v)));
+}
+
+struct PieceRing {
+  uint32_t a_lo, a_hi, pw, R, id;  // per lane: entry `lane`
+  uint32_t head, count;            // uniform
+  __device__ __forceinline__ void push(uint32_t l, uint64_t a0, uint32_t w, uint32_t reg,
+                                       uint32_t sid) {
+    const bool me = l == ((head + count) & 63u);
+    a_lo = me ? static_cast<uint32_t>(a0) : a_lo;
+    a_hi = me ? static_cast<uint32_t>(a0 >> 32) : a_hi;
+    pw = me ? w : pw;
+    R = me ? reg : R;
+    id = me ? sid : id;
+    ++count;
+  }
+};
+
+template <int OUT, typename Src>
+__device__ __forceinline__ void run_p(const Src& src, void* out, uint32_t flags,
+                                      const uint8_t* image) {
+  const uint32_t l = threadIdx.x & 63u;
+  const uint32_t w = uni(threadIdx.x >> 6);
+  const uint64_t count = src.count;
+  if (static_cast<uint64_t>(blockIdx.x) * 16u >= count) return;  // no block of work
+  load_image(image, w, l);
+  const Lane lk = make_lane<1>(l);
+  Pipe pp;
+  pp.init(l, w);
+  const bool msk = (flags & kFlagMask) != 0u;
+  const uint64_t sbase = reinterpret_cast<uint64_t>(src.base);
+
+  struct Pref {
+    SpanD d;
+    bool valid;
+  };
+  auto prefetch = [&](Pref& p) {
+    const uint64_t s = grab_units<1>(l);
+    p.valid = s < count;
+    if (p.valid) p.d = src.get(s);
+  };
+  auto issue = [&](const Seg& g) {
+    if (g.nc != 0u) pp.issue<4>(sbase + g.a0, 0u, kSegChunks, g.nc);
+    if ((g.flags & (kSegLast | kSegPiece)) == kSegLast)
+      pp.issue_end(sbase + g.a0 + 16u * g.nc, 0u, g.e > g.o, OUT == 1, g.e);
+  };
+  PieceRing ring{0, 0, 0, 0, 0, 0, 0};
+  // a batch of the ring's next n (<= 8) pieces: its DMAs
+  auto issue_batch = [&](uint32_t h0, uint32_t n) {
+#pragma unroll
+    for (uint32_t g = 0; g < 8; ++g) {
+      if (g >= n) break;
+      const uint32_t idx = (h0 + g) & 63u;
+      const uint64_t a0 = (static_cast<uint64_t>(uni(__builtin_amdgcn_readlane(ring.a_hi, idx))) << 32) |
+                          uni(__builtin_amdgcn_readlane(ring.a_lo, idx));
+      const uint32_t pw = uni(__builtin_amdgcn_readlane(ring.pw, idx));
+      const uint32_t nc = pw & 63u, e = (pw >> 8) & 15u;
+      const uint64_t base = sbase + a0;
+      if ((l >> 5) == (g & 1u)) {
+        // window chunk (cm mod 32) of the group is piece chunk (cm mod 32) - (32 - nc)
+        const int32_t b = 16 * (static_cast<int32_t>(pp.cm & 31u) - static_cast<int32_t>(32u - nc));
+        dma1nt(base, pp.slot + 1024u * (g >> 1), static_cast<uint32_t>(max(b, 0)));
+      }
+      pp.issue_end(base + 16u * nc, g, e != 0u, OUT == 1, e);
+    }
+  };
+
+  Walk wk;
+  Pref pf;
+  prefetch(pf);
+  if (!pf.valid) return;
+  wk.start(src.base, pf.d, true);
+  prefetch(pf);
+  Seg cur = wk.next();
+  issue(cur);
+  uint32_t chain = 0;  // register carried between the segments of a span
+  bool stored_prev = false;
+  g_u32* const out32 = (g_u32*)(reinterpret_cast<uintptr_t>(out));
+  g_u8* const out8 = (g_u8*)(reinterpret_cast<uintptr_t>(out));
+
+  for (;;) {
+    if (stored_prev) wait_vm<1>();
+    else wait_vm<0>();
+    uint32_t W[16];
+    pp.read(W);
+    // this lane's group's aux pieces (a segment: group 0)
+    const uint32_t grp = (cur.flags & kSegBatch) ? l >> 3 : 0u;
+    const u32x4 tl = pp.piece_lane(kAuxTail + grp);
+    const u32x4 nx = OUT == 1 ? pp.piece_lane(kAuxNext + grp) : u32x4{0, 0, 0, 0};
+    pp.release();
+    // the next iteration: a batch of 8 pieces, the rest of this span, or
+    // the prefetched span
+    Seg nxt;
+    nxt.flags = 0;
+    bool took_pf = false;
+    const bool more = wk.valid || pf.valid;
+    if (ring.count >= 8u || (ring.count != 0u && !more)) {
+      const uint32_t n = ring.count < 8u ? ring.count : 8u;
+      nxt.flags = kSegValid | kSegBatch;
+      nxt.init = ring.head;
+      nxt.nc = n;
+      issue_batch(ring.head, n);
+      ring.head = (ring.head + n) & 63u;
+      ring.count -= n;
+    } else if (more) {
+      if (!wk.valid) {
+        wk.start(src.base, pf.d, true);
+        took_pf = true;
+      }
+      nxt = wk.next();
+      issue(nxt);
+    }
+
+    bool did_store = false;
+    if (cur.flags & kSegBatch) {
+      // ---- a batch of pieces, one per 8-lane group ----
+      const uint32_t g = l >> 3, gl = l & 7u;
+      const uint32_t idx = (cur.init + g) & 63u;
+      const bool on = g < cur.nc;
+      const uint32_t pw = bperm(ring.pw, idx), reg = bperm(ring.R, idx);
+      const uint32_t nc = on ? pw & 63u : 0u, e = on ? (pw >> 8) & 15u : 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int32_t c = static_cast<int32_t>(4u * gl) + i - static_cast<int32_t>(32u - nc);
+#pragma unroll
+        for (uint32_t ww = 0; ww < 4; ++ww) W[4 * i + ww] &= c < 0 ? 0u : ~0u;
+        W[4 * i] ^= c == 0 ? reg : 0u;
+      }
+      uint32_t r = fold8(lk, l, scan(lk, W));
+      r = feed_tail_lanes(lk, l, r, tl, 0u, gl == 0u ? e : 0u);
+      const uint32_t crc = ~r;
+      const uint32_t sid = bperm(ring.id, idx);
+      if (gl == 0u && on) {
+        if (OUT == 1) out8[sid] = unmask_crc(le32_at(tl, nx, e)) == crc ? 1u : 0u;
+        else out32[sid] = msk ? mask_crc(crc) : crc;
+      }
+      did_store = true;
+    } else {
+      // ---- CRC of the current segment ----
+      uint32_t R;
+      if (cur.nc == 0u) {
+        R = ~cur.init;  // a span inside one chunk: all of it is tail
+      } else {
+        const uint32_t inj = (cur.flags & kSegFirst) ? head_register(l, cur.init, cur.h) : chain;
+        if (cur.nc == kSegChunks && cur.h == 0u) {
+          W[0] ^= l == 0u ? inj : 0u;
+        } else {
+          // chunk i of lane l is segment chunk 4l + i - (256 - nc): zero the
+          // ones in front of the segment, mask the first h bytes of chunk 0
+          // and put the register there
+          const int32_t base = static_cast<int32_t>(kSegChunks - cur.nc);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int32_t ci = static_cast<int32_t>(4u * l) + i - base;
+#pragma unroll
+            for (uint32_t ww = 0; ww < 4; ++ww)
+              W[4 * i + ww] &= ci < 0 ? 0u : (ci == 0 ? head_mask(cur.h, ww) : ~0u);
+            W[4 * i] ^= ci == 0 ? inj : 0u;
+          }
+        }
+        R = fold<1>(lk, l, scan(lk, W))[0];
+      }
+      if (cur.flags & kSegPiece) {
+        // the rest goes to the ring, continuing from R
+        ring.push(l, cur.a0 + kSegChunks * 16u, cur.pw, R, static_cast<uint32_t>(cur.id));
+      } else if (cur.flags & kSegLast) {
+        const u32x4 t{uni(tl.x), uni(tl.y), uni(tl.z), uni(tl.w)};
+        if (cur.e > cur.o) R = feed_tail(lk, l, R, t, cur.o, cur.e);
+        const uint32_t crc = ~R;
+        did_store = true;
+        if (l == 0u) {
+          if (OUT == 1) out8[cur.id] = unmask_crc(le32_at(t, nx, cur.e)) == crc ? 1u : 0u;
+          else out32[cur.id] = msk ? mask_crc(crc) : crc;
+        }
+      } else {
+        chain = R;
+      }
+    }
+    stored_prev = did_store;
+
+    if (!(nxt.flags & kSegValid)) {
+      if (ring.count == 0u) break;
+      // the last pieces, pushed by this iteration: their DMAs go out after
+      // its store, so the next wait is for everything
+      const uint32_t n = ring.count;
+      nxt.flags = kSegValid | kSegBatch;
+      nxt.init = ring.head;
+      nxt.nc = n;
+      issue_batch(ring.head, n);
+      ring.head = (ring.head + n) & 63u;
+      ring.count = 0;
+      stored_prev = false;
+    }
     if (took_pf) prefetch(pf);
     cur = nxt;
   }
@@ -893,7 +1131,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const DescSrc src{base, offsets, lengths, inits, count, 0u};
-  run1<0>(src, out, flags, nullptr, nullptr, image);
+  run_p<0>(src, out, flags, image);
 }
 
 // Fixed-size blocks at a fixed stride.
@@ -901,7 +1139,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t length, uint32_t init,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const StridedSrc src{base, stride, length, init, count};
-  run1<0>(src, out, flags & kFlagMask, nullptr, nullptr, image);
+  run_p<0>(src, out, flags & kFlagMask, image);
 }
 
 // Read-side verify (ReadBlock, kv/src/table/format.cc:91-99): block i =
@@ -912,7 +1150,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
     const uint8_t* __restrict__ image) {
   const DescSrc src{base, offsets, lengths, nullptr, count, 1u};
-  run1<1>(src, status, 0u, nullptr, nullptr, image);
+  run_p<1>(src, status, 0u, image);
 }
 
 // A size-class list (HCRC_SPLIT_SMALL): G = 1 takes the spans of more than
