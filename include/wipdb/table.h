@@ -38,6 +38,51 @@ enum class CrcMode {
   kBatchAuto = 3,  // deferred and batched; MI355X when usable, else host
 };
 
+// The table-side methods of kv::Comparator (kv/src/include/kv/comparator.h:
+// 18-70): the builder shortens index keys with them.
+class Comparator {
+ public:
+  virtual ~Comparator() = default;
+  virtual const char* Name() const = 0;
+  virtual int Compare(std::string_view a, std::string_view b) const = 0;
+  // If *start < limit, changes *start to a short key in [start, limit).
+  virtual void FindShortestSeparator(std::string* start, std::string_view limit) const = 0;
+  // Changes *key to a short key >= *key.
+  virtual void FindShortSuccessor(std::string* key) const = 0;
+};
+
+// kv::BytewiseComparator() (kv/src/util/comparator.cc:22-96).
+const Comparator* BytewiseComparator();
+
+// kv::InternalKeyComparator (kv/src/db/dbformat.cc:45-120): keys are
+// user_key || fixed64(sequence << 8 | type); order is user key ascending
+// (by `user`), then sequence descending.  A shortened user key gets the tag
+// (kMaxSequenceNumber, kValueTypeForSeek).  This is the comparator WipDB's
+// flush and compaction build every SST with (SanitizeOptions,
+// kv/src/db/db_impl.cc:104-111,141-144).
+class InternalKeyComparator : public Comparator {
+ public:
+  explicit InternalKeyComparator(const Comparator* user) : user_(user) {}
+  const char* Name() const override;
+  int Compare(std::string_view a, std::string_view b) const override;
+  void FindShortestSeparator(std::string* start, std::string_view limit) const override;
+  void FindShortSuccessor(std::string* key) const override;
+  const Comparator* user_comparator() const { return user_; }
+
+ private:
+  const Comparator* user_;
+};
+
+// InternalKeyComparator(BytewiseComparator()), process-lifetime.
+const Comparator* InternalBytewiseComparator();
+
+// Which bytes of a key the bloom filter hashes.
+enum class FilterKeys {
+  kWholeKey = 0,  // NewBloomFilterPolicy used directly (kv::Options default)
+  kUserKey = 1,   // InternalFilterPolicy: ExtractUserKey(key), the 8-byte tag
+                  // stripped (kv/src/db/dbformat.cc:122-136)
+};
+
 struct TableOptions {
   size_t block_size = 4096;          // kv/src/util/options.cc:22
   int block_restart_interval = 16;   // options.cc:23
@@ -45,7 +90,14 @@ struct TableOptions {
   size_t max_buffer_size = 4u << 20; // EnvOptions::writable_file_max_buffer_size (env.h:85)
   CrcMode crc_mode = CrcMode::kBatchAuto;
   int device = 0;                    // HIP device for the batched modes
+  const Comparator* comparator = nullptr;  // nullptr: BytewiseComparator()
+  FilterKeys filter_keys = FilterKeys::kWholeKey;
 };
+
+// The options WipDB's DB hands its TableBuilders (BuildTableKV,
+// kv/src/db/builder.cc:46, and compaction outputs): internal keys over the
+// bytewise user comparator, the bloom filter wrapped in InternalFilterPolicy.
+TableOptions InternalKeyTableOptions(TableOptions base);
 
 // Destination of a table's bytes (the WritableFileWriter role).
 class TableSink {
@@ -70,7 +122,7 @@ class TableBuilder {
   TableBuilder(const TableBuilder&) = delete;
   TableBuilder& operator=(const TableBuilder&) = delete;
 
-  // REQUIRES: key > every key added before (bytewise).
+  // REQUIRES: key > every key added before (in options.comparator's order).
   void Add(std::string_view key, std::string_view value);
   void Flush();
   Status Finish();

@@ -53,6 +53,24 @@ int wsst_build_tables(size_t ntables, const size_t* entries, const char* keys,
                       size_t cap, uint64_t* out_offsets, uint64_t* sizes,
                       uint64_t* batched_blocks);
 
+/* Key formats of wsst_build_tables_ex.
+ *   WSST_KEYS_BYTEWISE  kv::Options defaults: BytewiseComparator, raw bloom keys
+ *   WSST_KEYS_INTERNAL  WipDB's DB tables: InternalKeyComparator(Bytewise) and
+ *                       InternalFilterPolicy (kv/src/db/db_impl.cc:141-144,
+ *                       dbformat.cc:89-136); every key carries the 8-byte tag */
+#define WSST_KEYS_BYTEWISE 0
+#define WSST_KEYS_INTERNAL 1
+
+/* wsst_build_tables with a key format: WSST_KEYS_INTERNAL writes the index
+ * separators and bloom filters of the tables WipDB's flush (BuildTableKV,
+ * kv/src/db/builder.cc:46-54) and compaction produce. */
+int wsst_build_tables_ex(size_t ntables, const size_t* entries, const char* keys,
+                         const uint32_t* key_lens, const char* vals, const uint32_t* val_lens,
+                         int block_size, int restart_interval, int bloom_bits,
+                         size_t max_buffer_size, int crc_mode, int device, int key_format,
+                         char* out, size_t cap, uint64_t* out_offsets, uint64_t* sizes,
+                         uint64_t* batched_blocks);
+
 /* ReadBlock(verify_checksums) on a table image (kv/src/table/format.cc:66). */
 int wsst_read_block(const char* image, size_t n, uint64_t offset, uint64_t size);
 

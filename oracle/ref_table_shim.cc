@@ -5,6 +5,8 @@
 //   kv::TableBuilder           kv/src/table/table_builder.cc:66-271
 //   kv::Table::Open / ReadBlock kv/src/table/table.cc:37-82, format.cc:66-143
 //   kv::NewBloomFilterPolicy   kv/src/table/bloom.cc:88-90
+//   kv::InternalKeyComparator, kv::InternalFilterPolicy  kv/src/db/dbformat.cc:45-136
+//     (the options WipDB's DB builds every SST with, db_impl.cc:141-144)
 // It writes SSTs into memory (an in-memory kv::WritableFile behind the
 // reference's WritableFileWriter) so the tests can byte-compare the batched
 // table builder's output with the reference's, and it reads them back
@@ -16,6 +18,8 @@
 
 #include <string>
 
+#include "db/dbformat.h"
+#include "kv/comparator.h"
 #include "kv/env.h"
 #include "kv/filter_policy.h"
 #include "kv/options.h"
@@ -73,16 +77,25 @@ extern "C" {
 
 // Builds one table from n sorted (key, value) pairs (concatenated blobs +
 // lengths) with the reference TableBuilder.  bloom_bits <= 0: no filter.
-// Writes at most cap bytes of the table to out; returns the table size, or
-// -1 on a builder error.
-long ref_build_table(const char* keys, const uint32_t* key_lens, const char* vals,
-                     const uint32_t* val_lens, size_t n, int block_size,
-                     int restart_interval, int bloom_bits, char* out, size_t cap) {
+// internal != 0: the DB's options -- InternalKeyComparator(BytewiseComparator)
+// and InternalFilterPolicy around the bloom policy (SanitizeOptions,
+// kv/src/db/db_impl.cc:104-111).  Writes at most cap bytes of the table to
+// out; returns the table size, or -1 on a builder error.
+long ref_build_table_ex(const char* keys, const uint32_t* key_lens, const char* vals,
+                        const uint32_t* val_lens, size_t n, int block_size,
+                        int restart_interval, int bloom_bits, int internal, char* out,
+                        size_t cap) {
   kv::Options opt;
   opt.block_size = static_cast<size_t>(block_size);
   opt.block_restart_interval = restart_interval;
   const kv::FilterPolicy* fp = bloom_bits > 0 ? kv::NewBloomFilterPolicy(bloom_bits) : nullptr;
+  kv::InternalKeyComparator icmp(kv::BytewiseComparator());
+  kv::InternalFilterPolicy ipolicy(fp);
   opt.filter_policy = fp;
+  if (internal) {
+    opt.comparator = &icmp;
+    opt.filter_policy = fp ? &ipolicy : nullptr;
+  }
   MemWritable* mf = new MemWritable;
   long rc = -1;
   {
@@ -104,6 +117,32 @@ long ref_build_table(const char* keys, const uint32_t* key_lens, const char* val
   }  // ~WritableFileWriter closes (and owns) the file
   delete fp;
   return rc;
+}
+
+long ref_build_table(const char* keys, const uint32_t* key_lens, const char* vals,
+                     const uint32_t* val_lens, size_t n, int block_size,
+                     int restart_interval, int bloom_bits, char* out, size_t cap) {
+  return ref_build_table_ex(keys, key_lens, vals, val_lens, n, block_size, restart_interval,
+                            bloom_bits, 0, out, cap);
+}
+
+// kv::InternalKeyComparator(BytewiseComparator) on two keys: <0, 0, >0.
+int ref_internal_compare(const char* a, size_t an, const char* b, size_t bn) {
+  kv::InternalKeyComparator icmp(kv::BytewiseComparator());
+  return icmp.Compare(kv::Slice(a, an), kv::Slice(b, bn));
+}
+
+// Bloom KeyMayMatch of the table's filter for `key` through the reference's
+// Table::InternalGet path is not exposed; instead this returns the filter
+// policy's verdict on a filter blob (InternalFilterPolicy when internal).
+int ref_filter_may_match(const char* filter, size_t fn, const char* key, size_t kn,
+                         int bloom_bits, int internal) {
+  const kv::FilterPolicy* fp = kv::NewBloomFilterPolicy(bloom_bits);
+  kv::InternalFilterPolicy ipolicy(fp);
+  const kv::FilterPolicy* use = internal ? static_cast<const kv::FilterPolicy*>(&ipolicy) : fp;
+  const int r = use->KeyMayMatch(kv::Slice(key, kn), kv::Slice(filter, fn)) ? 1 : 0;
+  delete fp;
+  return r;
 }
 
 // Opens a table image with Table::Open (paranoid_checks: the index block is

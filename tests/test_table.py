@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -22,6 +23,7 @@ from wipdb_amd import sst
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_TABLE_SO = os.path.join(REPO, "oracle", "_ref", "libref_table.so")
+KV_BUILDER_TEST = os.path.join(REPO, "oracle", "_ref", "test_kv_builder")
 
 
 class RefTable:
@@ -33,13 +35,21 @@ class RefTable:
         lib.ref_build_table.restype = ctypes.c_long
         lib.ref_build_table.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, vp, sz]
+        lib.ref_build_table_ex.restype = ctypes.c_long
+        lib.ref_build_table_ex.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, vp, sz]
+        lib.ref_internal_compare.restype = ctypes.c_int
+        lib.ref_internal_compare.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
+        lib.ref_filter_may_match.restype = ctypes.c_int
+        lib.ref_filter_may_match.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz,
+                                             ctypes.c_int, ctypes.c_int]
         lib.ref_verify_table.restype = ctypes.c_int
         lib.ref_verify_table.argtypes = [vp, sz, ctypes.c_int, ctypes.POINTER(sz)]
         lib.ref_read_block.restype = ctypes.c_int
         lib.ref_read_block.argtypes = [vp, sz, ctypes.c_uint64, ctypes.c_uint64]
         self.lib = lib
 
-    def build(self, kvs, block_size=4096, restart=16, bloom=0) -> bytes:
+    def build(self, kvs, block_size=4096, restart=16, bloom=0, internal=False) -> bytes:
         keys = b"".join(k for k, _ in kvs)
         vals = b"".join(v for _, v in kvs)
         kl = np.array([len(k) for k, _ in kvs] or [0], np.uint32)
@@ -48,8 +58,8 @@ class RefTable:
         out = ctypes.create_string_buffer(cap)
         kb = ctypes.create_string_buffer(keys, len(keys) or 1)
         vb = ctypes.create_string_buffer(vals, len(vals) or 1)
-        n = self.lib.ref_build_table(kb, kl.ctypes.data, vb, vl.ctypes.data, len(kvs),
-                                     block_size, restart, bloom, out, cap)
+        n = self.lib.ref_build_table_ex(kb, kl.ctypes.data, vb, vl.ctypes.data, len(kvs),
+                                        block_size, restart, bloom, int(internal), out, cap)
         assert 0 < n <= cap
         return out.raw[:n]
 
@@ -111,6 +121,33 @@ def kv_mixed(n: int, seed: int):
     return out
 
 
+def _tag(seq: int, typ: int) -> bytes:
+    """PackSequenceAndType (kv/src/db/dbformat.cc:12-16), fixed64."""
+    return ((seq << 8) | typ).to_bytes(8, "little")
+
+
+def kv_internal(n: int, seed: int, dup: bool = True):
+    """Internal keys as a flush / compaction writes them: user keys of every
+    shape kv_mixed makes (0xff runs, shared prefixes, keys that are prefixes
+    of others), each with 1..3 versions (sequence descending, puts and
+    deletions), ordered by InternalKeyComparator(BytewiseComparator)."""
+    rng = np.random.default_rng(seed)
+    users = sorted({k for k, _ in kv_mixed(n, seed + 1000)} | {b"ab", b"abc", b"abd", b"b"})
+    out, seq = [], 1 << 40
+    for u in users:
+        for _ in range(int(rng.integers(1, 4)) if dup else 1):
+            seq -= int(rng.integers(1, 1000))
+            typ = 0 if rng.random() < 0.1 else 1
+            vl = 0 if typ == 0 else int(rng.integers(1, 300))
+            out.append((u + _tag(seq, typ), bytes(rng.integers(0, 256, size=vl, dtype=np.uint8))))
+    return out
+
+
+def kv_8binsert_internal(n: int, seed: int):
+    """8Binsert's DB tables: 16-byte hex user keys + tag, 100-byte values."""
+    return kv_8binsert(n, seed)
+
+
 CONFIGS = [
     # (stream, n, seed, block_size, restart, bloom, max_buffer)
     ("8binsert", 6000, 1, 4096, 16, 10, 4 << 20),
@@ -153,6 +190,111 @@ def test_finish_tables_matches_one_by_one(ref_table):
     for t, img in zip(tables, imgs):
         assert img == ref_table.build(t, bloom=10)
     assert batched == sum(len(_handles(img)) for img in imgs)
+
+
+# ---- WipDB's DB tables: internal keys (db_impl.cc:141-144) -------------------
+
+INTERNAL_CONFIGS = [
+    # (stream, n, seed, block_size, restart, bloom)
+    ("internal", 3000, 51, 4096, 16, 10),
+    ("internal", 3000, 52, 1024, 4, 10),
+    ("internal", 2000, 53, 256, 1, 7),
+    ("8binsert", 6000, 54, 4096, 16, 10),
+    ("8binsert", 6000, 55, 4096, 16, 0),
+    ("internal", 1, 56, 4096, 16, 10),
+]
+
+
+def _istream(kind, n, seed):
+    return kv_8binsert_internal(n, seed) if kind == "8binsert" else kv_internal(n, seed)
+
+
+def test_internal_comparator_order_matches_reference(ref_table):
+    """The streams are sorted the way the reference's InternalKeyComparator
+    sorts them (user key ascending, sequence descending)."""
+    kvs = kv_internal(1500, 50)
+    for (a, _), (b, _) in zip(kvs, kvs[1:]):
+        assert ref_table.lib.ref_internal_compare(a, len(a), b, len(b)) < 0
+
+
+@pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
+@pytest.mark.parametrize("cfg", INTERNAL_CONFIGS,
+                         ids=[f"{c[0]}-{c[1]}-b{c[3]}-r{c[4]}-f{c[5]}" for c in INTERNAL_CONFIGS])
+def test_internal_key_tables_equal_reference(ref_table, cfg, mode):
+    """Byte parity with kv::TableBuilder under the DB's options:
+    InternalKeyComparator separators / successors (the shortened user key +
+    (kMaxSequenceNumber, kValueTypeForSeek)) and user-key bloom filters."""
+    kind, n, seed, bs, rs, bloom = cfg
+    kvs = _istream(kind, n, seed)
+    want = ref_table.build(kvs, bs, rs, bloom, internal=True)
+    rc, imgs, batched = sst.build_tables([kvs], bs, rs, bloom, crc_mode=mode,
+                                         key_format=sst.KEYS_INTERNAL)
+    assert rc == sst.OK
+    assert imgs[0] == want
+    assert ref_table.verify(imgs[0], bloom) == 0
+
+
+def test_internal_key_format_changes_index_and_filter(ref_table):
+    """The internal-key options are not the default ones: the same stream
+    built bytewise has different index separators and filter bits (so a
+    bytewise-only builder would not be a drop-in for the DB's tables).  The
+    8Binsert shape (fixed-size unique user keys) is sorted in both orders."""
+    kvs = kv_8binsert(3000, 57)
+    a = ref_table.build(kvs, bloom=10, internal=True)
+    b = ref_table.build(kvs, bloom=10, internal=False)
+    assert a != b
+    _, (ia,), _ = sst.build_tables([kvs], bloom_bits=10, crc_mode=sst.CRC_BATCH_CPU,
+                                   key_format=sst.KEYS_INTERNAL)
+    _, (ib,), _ = sst.build_tables([kvs], bloom_bits=10, crc_mode=sst.CRC_BATCH_CPU)
+    assert ia == a and ib == b
+
+
+def test_internal_key_filter_matches_user_keys(ref_table):
+    """The filter block of an internal-key table answers KeyMayMatch for every
+    user key under the reference's InternalFilterPolicy (any tag)."""
+    kvs = kv_internal(800, 58)
+    _, (img,), _ = sst.build_tables([kvs], bloom_bits=10, crc_mode=sst.CRC_BATCH_CPU,
+                                    key_format=sst.KEYS_INTERNAL)
+    hs = _handles(img)
+    fo, fs = hs[-1]  # the filter block (last handle found in the meta-index)
+    blob = img[fo:fo + fs]
+    # one 2 KiB-granular filter per data block start; the first filter covers
+    # the first block's keys -- check them with the policy directly
+    nf = (len(blob) - int.from_bytes(blob[-5:-1], "little") - 1) // 4
+    off0 = int.from_bytes(blob[-5:-1], "little")
+    first = blob[int.from_bytes(blob[off0:off0 + 4], "little"):
+                 int.from_bytes(blob[off0 + 4:off0 + 8], "little") if nf > 1 else off0]
+    k0 = kvs[0][0]
+    other_tag = k0[:-8] + _tag(1, 1)
+    for key in (k0, other_tag):
+        assert ref_table.lib.ref_filter_may_match(first, len(first), key, len(key), 10, 1) == 1
+
+
+@pytest.mark.parametrize("mode", [sst.CRC_BATCH_CPU])
+def test_internal_key_compaction_outputs_one_batch(ref_table, mode):
+    kvs = kv_internal(6000, 59)
+    tables = [kvs[i:i + 1100] for i in range(0, len(kvs), 1100)]
+    rc, imgs, _ = sst.build_tables(tables, bloom_bits=10, crc_mode=mode,
+                                   key_format=sst.KEYS_INTERNAL)
+    assert rc == sst.OK
+    for t, img in zip(tables, imgs):
+        assert img == ref_table.build(t, bloom=10, internal=True)
+
+
+def _run_kv_builder(mode: int):
+    """tests/cpp/test_kv_builder.cc: the patched BuildTableKV / compaction
+    (kvcompat::WritableFileWriterSink over kv::WritableFileWriter) against
+    kv::TableBuilder under the DB's options, and kv::Table reading it back."""
+    if not os.path.exists(KV_BUILDER_TEST):
+        pytest.skip("oracle/_ref/test_kv_builder not built (reference absent)")
+    r = subprocess.run([KV_BUILDER_TEST, str(mode)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "6 identical" in r.stdout and "identical" in r.stdout.splitlines()[0]
+
+
+@pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
+def test_kv_builder_integration(mode):
+    _run_kv_builder(mode)
 
 
 # ---- read side --------------------------------------------------------------
@@ -310,3 +452,35 @@ def test_gpu_verify_matches_reference(ref_table, engine):
             imgs.append(bytes(b))
     rc, codes = sst.verify_tables(imgs, 10, sst.CRC_BATCH_GPU)
     assert codes == [ref_table.verify(i, 10) for i in imgs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", INTERNAL_CONFIGS[:4],
+                         ids=[f"{c[0]}-{c[1]}-b{c[3]}" for c in INTERNAL_CONFIGS[:4]])
+def test_gpu_internal_key_tables_equal_reference(ref_table, cfg, engine):
+    """WipDB's DB tables (internal keys, InternalFilterPolicy) with every
+    block CRC computed on the MI355X: bytes equal the reference's."""
+    kind, n, seed, bs, rs, bloom = cfg
+    kvs = _istream(kind, n, seed)
+    rc, imgs, batched = sst.build_tables([kvs], bs, rs, bloom, crc_mode=sst.CRC_BATCH_GPU,
+                                         key_format=sst.KEYS_INTERNAL)
+    assert rc == sst.OK and batched > 0
+    assert imgs[0] == ref_table.build(kvs, bs, rs, bloom, internal=True)
+
+
+@pytest.mark.gpu
+def test_gpu_internal_key_compaction_outputs(ref_table, engine):
+    """A compaction's 16 internal-key output tables finished in one MI355X batch."""
+    kvs = kv_internal(16 * 700, 60)
+    tables = [kvs[i:i + 700] for i in range(0, len(kvs), 700)]
+    rc, imgs, batched = sst.build_tables(tables, bloom_bits=10, crc_mode=sst.CRC_BATCH_GPU,
+                                         key_format=sst.KEYS_INTERNAL)
+    assert rc == sst.OK and batched > 0
+    for t, img in zip(tables, imgs):
+        assert img == ref_table.build(t, bloom=10, internal=True)
+
+
+@pytest.mark.gpu
+def test_gpu_kv_builder_integration(engine):
+    """The reference-side integration with every block CRC on the MI355X."""
+    _run_kv_builder(sst.CRC_BATCH_GPU)

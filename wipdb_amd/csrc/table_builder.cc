@@ -47,8 +47,86 @@ namespace table {
 
 using sst::Handle;
 
+namespace {
+
+class Bytewise : public Comparator {
+ public:
+  const char* Name() const override { return "leveldb.BytewiseComparator"; }
+  int Compare(std::string_view a, std::string_view b) const override { return a.compare(b); }
+  void FindShortestSeparator(std::string* start, std::string_view limit) const override {
+    sst::ShortestSeparator(start, limit);
+  }
+  void FindShortSuccessor(std::string* key) const override { sst::ShortSuccessor(key); }
+};
+
+// dbformat.h:74-75, 68: the tag a shortened internal key gets
+constexpr uint64_t kMaxSequenceNumber = (uint64_t(1) << 56) - 1;
+constexpr uint64_t kValueTypeForSeek = 1;  // kTypeValue
+
+void PutFixed64(std::string* d, uint64_t v) {
+  sst::PutFixed32(d, static_cast<uint32_t>(v));
+  sst::PutFixed32(d, static_cast<uint32_t>(v >> 32));
+}
+uint64_t DecodeFixed64(const char* p) {
+  return uint64_t(sst::DecodeFixed32(p)) | (uint64_t(sst::DecodeFixed32(p + 4)) << 32);
+}
+// ExtractUserKey (dbformat.h:96-99); keys shorter than the tag are kept
+// whole (the reference asserts size >= 8)
+std::string_view UserKey(std::string_view k) { return k.size() >= 8 ? k.substr(0, k.size() - 8) : k; }
+
+}  // namespace
+
+const Comparator* BytewiseComparator() {
+  static const Bytewise* c = new Bytewise;
+  return c;
+}
+
+const char* InternalKeyComparator::Name() const { return "leveldb.InternalKeyComparator"; }
+
+int InternalKeyComparator::Compare(std::string_view a, std::string_view b) const {
+  int r = user_->Compare(UserKey(a), UserKey(b));
+  if (r == 0 && a.size() >= 8 && b.size() >= 8) {
+    const uint64_t an = DecodeFixed64(a.data() + a.size() - 8);
+    const uint64_t bn = DecodeFixed64(b.data() + b.size() - 8);
+    r = an > bn ? -1 : (an < bn ? 1 : 0);  // larger sequence first
+  }
+  return r;
+}
+
+void InternalKeyComparator::FindShortestSeparator(std::string* start, std::string_view limit) const {
+  const std::string_view us = UserKey(*start);
+  std::string tmp(us);
+  user_->FindShortestSeparator(&tmp, UserKey(limit));
+  if (tmp.size() < us.size() && user_->Compare(us, tmp) < 0) {
+    PutFixed64(&tmp, (kMaxSequenceNumber << 8) | kValueTypeForSeek);
+    start->swap(tmp);
+  }
+}
+
+void InternalKeyComparator::FindShortSuccessor(std::string* key) const {
+  const std::string_view uk = UserKey(*key);
+  std::string tmp(uk);
+  user_->FindShortSuccessor(&tmp);
+  if (tmp.size() < uk.size() && user_->Compare(uk, tmp) < 0) {
+    PutFixed64(&tmp, (kMaxSequenceNumber << 8) | kValueTypeForSeek);
+    key->swap(tmp);
+  }
+}
+
+const Comparator* InternalBytewiseComparator() {
+  static const InternalKeyComparator* c = new InternalKeyComparator(BytewiseComparator());
+  return c;
+}
+
+TableOptions InternalKeyTableOptions(TableOptions base) {
+  base.comparator = InternalBytewiseComparator();
+  base.filter_keys = FilterKeys::kUserKey;
+  return base;
+}
+
 struct TableBuilder::Rep {
   TableOptions opt;
+  const Comparator* cmp;
   TableSink* sink;
   uint64_t offset = 0;  // file offset of the next byte
   Status status;
@@ -68,7 +146,11 @@ struct TableBuilder::Rep {
   uint64_t batched_blocks = 0;
 
   Rep(const TableOptions& o, TableSink* s)
-      : opt(o), sink(s), data_block(o.block_restart_interval), index_block(1) {
+      : opt(o),
+        cmp(o.comparator ? o.comparator : BytewiseComparator()),
+        sink(s),
+        data_block(o.block_restart_interval),
+        index_block(1) {
     if (o.bloom_bits_per_key > 0) {
       filter.reset(new sst::FilterBuilder(o.bloom_bits_per_key));
       filter->StartBlock(0);
@@ -161,7 +243,7 @@ struct TableBuilder::Rep {
     }
     if (status.ok()) {
       if (pending_index_entry) {
-        sst::ShortSuccessor(&last_key);
+        cmp->FindShortSuccessor(&last_key);
         std::string enc;
         pending_handle.EncodeTo(&enc);
         index_block.Add(last_key, enc);
@@ -187,13 +269,13 @@ void TableBuilder::Add(std::string_view key, std::string_view value) {
   Rep* r = rep_;
   if (r->closed || !r->status.ok()) return;
   if (r->pending_index_entry) {
-    sst::ShortestSeparator(&r->last_key, key);
+    r->cmp->FindShortestSeparator(&r->last_key, key);
     std::string enc;
     r->pending_handle.EncodeTo(&enc);
     r->index_block.Add(r->last_key, enc);
     r->pending_index_entry = false;
   }
-  if (r->filter) r->filter->AddKey(key);
+  if (r->filter) r->filter->AddKey(r->opt.filter_keys == FilterKeys::kUserKey ? UserKey(key) : key);
   r->last_key.assign(key.data(), key.size());
   ++r->num_entries;
   r->data_block.Add(key, value);

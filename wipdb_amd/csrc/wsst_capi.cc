@@ -40,9 +40,21 @@ int wsst_build_tables(size_t ntables, const size_t* entries, const char* keys,
                       size_t max_buffer_size, int crc_mode, int device, char* out,
                       size_t cap, uint64_t* out_offsets, uint64_t* sizes,
                       uint64_t* batched_blocks) {
+  return wsst_build_tables_ex(ntables, entries, keys, key_lens, vals, val_lens, block_size,
+                              restart_interval, bloom_bits, max_buffer_size, crc_mode, device,
+                              WSST_KEYS_BYTEWISE, out, cap, out_offsets, sizes, batched_blocks);
+}
+
+int wsst_build_tables_ex(size_t ntables, const size_t* entries, const char* keys,
+                         const uint32_t* key_lens, const char* vals, const uint32_t* val_lens,
+                         int block_size, int restart_interval, int bloom_bits,
+                         size_t max_buffer_size, int crc_mode, int device, int key_format,
+                         char* out, size_t cap, uint64_t* out_offsets, uint64_t* sizes,
+                         uint64_t* batched_blocks) {
   CrcMode mode;
   if (!ModeOf(crc_mode, &mode) || !entries || !out || !out_offsets || !sizes ||
-      block_size <= 0 || restart_interval <= 0 || max_buffer_size == 0)
+      block_size <= 0 || restart_interval <= 0 || max_buffer_size == 0 ||
+      (key_format != WSST_KEYS_BYTEWISE && key_format != WSST_KEYS_INTERNAL))
     return WSST_ERR_INVALID;
   wipdb::table::TableOptions opt;
   opt.block_size = static_cast<size_t>(block_size);
@@ -51,6 +63,7 @@ int wsst_build_tables(size_t ntables, const size_t* entries, const char* keys,
   opt.max_buffer_size = max_buffer_size;
   opt.crc_mode = mode;
   opt.device = device;
+  if (key_format == WSST_KEYS_INTERNAL) opt = wipdb::table::InternalKeyTableOptions(opt);
   std::vector<std::unique_ptr<wipdb::table::StringSink>> sinks(ntables);
   std::vector<std::unique_ptr<wipdb::table::TableBuilder>> tbs(ntables);
   std::vector<wipdb::table::TableBuilder*> raw(ntables);

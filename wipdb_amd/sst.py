@@ -28,12 +28,16 @@ HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__fil
 OK, CORRUPTION, CRC_MISMATCH, OTHER = 0, 1, 2, 3
 ERR_INVALID, ERR_TOO_SMALL, ERR_DEVICE = -1, -2, -3
 CRC_INLINE, CRC_BATCH_CPU, CRC_BATCH_GPU, CRC_BATCH_AUTO = 0, 1, 2, 3
+KEYS_BYTEWISE, KEYS_INTERNAL = 0, 1
 
 _c = ctypes
 _vp, _sz = _c.c_void_p, _c.c_size_t
 _PROTOS = {
     "wsst_build_tables": (_c.c_int, [_sz, _vp, _vp, _vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int,
                                      _sz, _c.c_int, _c.c_int, _vp, _sz, _vp, _vp, _vp]),
+    "wsst_build_tables_ex": (_c.c_int, [_sz, _vp, _vp, _vp, _vp, _vp, _c.c_int, _c.c_int,
+                                        _c.c_int, _sz, _c.c_int, _c.c_int, _c.c_int, _vp, _sz,
+                                        _vp, _vp, _vp]),
     "wsst_read_block": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64]),
     "wsst_verify_tables": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_int, _c.c_int, _vp, _vp,
                                       _vp]),
@@ -77,21 +81,23 @@ def _blob(items: Sequence[bytes]):
 def build_tables(tables: Sequence[Sequence[tuple[bytes, bytes]]], block_size: int = 4096,
                  restart_interval: int = 16, bloom_bits: int = 0,
                  max_buffer_size: int = 4 << 20, crc_mode: int = CRC_BATCH_AUTO,
-                 device: int = 0) -> tuple[int, list[bytes], int]:
+                 device: int = 0, key_format: int = KEYS_BYTEWISE) -> tuple[int, list[bytes], int]:
     """Builds every table (a sorted list of (key, value)) and finishes them
-    together.  Returns (status code, table images, blocks CRC'd in batches)."""
+    together.  Returns (status code, table images, blocks CRC'd in batches).
+    key_format=KEYS_INTERNAL: WipDB's DB tables (internal keys with their
+    8-byte tag, InternalKeyComparator + InternalFilterPolicy)."""
     entries = np.array([len(t) for t in tables], dtype=np.uint64)
     flat = [kv for t in tables for kv in t]
     keys, klen = _blob([k for k, _ in flat])
     vals, vlen = _blob([v for _, v in flat])
     return build_tables_raw(entries, keys, klen, vals, vlen, block_size, restart_interval,
-                            bloom_bits, max_buffer_size, crc_mode, device)
+                            bloom_bits, max_buffer_size, crc_mode, device, key_format)
 
 
 def build_tables_raw(entries, keys: bytes, klen, vals: bytes, vlen, block_size: int = 4096,
                      restart_interval: int = 16, bloom_bits: int = 0,
                      max_buffer_size: int = 4 << 20, crc_mode: int = CRC_BATCH_AUTO,
-                     device: int = 0) -> tuple[int, list[bytes], int]:
+                     device: int = 0, key_format: int = KEYS_BYTEWISE) -> tuple[int, list[bytes], int]:
     """build_tables over pre-packed blobs: entries[t] pairs for table t, keys
     and values concatenated with their uint32 lengths."""
     lib = _load()
@@ -108,13 +114,13 @@ def build_tables_raw(entries, keys: bytes, klen, vals: bytes, vlen, block_size: 
     vbuf = _c.create_string_buffer(vals, len(vals) or 1)
     global last_call_seconds
     t0 = time.perf_counter()
-    rc = lib.wsst_build_tables(n, entries.ctypes.data, kbuf, klen.ctypes.data, vbuf,
-                               vlen.ctypes.data, block_size, restart_interval, bloom_bits,
-                               max_buffer_size, crc_mode, device, out, cap, offs.ctypes.data,
-                               sizes.ctypes.data, _c.byref(batched))
+    rc = lib.wsst_build_tables_ex(n, entries.ctypes.data, kbuf, klen.ctypes.data, vbuf,
+                                  vlen.ctypes.data, block_size, restart_interval, bloom_bits,
+                                  max_buffer_size, crc_mode, device, key_format, out, cap,
+                                  offs.ctypes.data, sizes.ctypes.data, _c.byref(batched))
     last_call_seconds = time.perf_counter() - t0
     if rc < 0:
-        raise SstError(f"wsst_build_tables: {rc}")
+        raise SstError(f"wsst_build_tables_ex: {rc}")
     raw = out.raw
     imgs = [raw[int(offs[i]):int(offs[i] + sizes[i])] for i in range(n)]
     return rc, imgs, int(batched.value)
