@@ -54,9 +54,20 @@ def dev(a, d):
     return torch.from_numpy(a).to(d)
 
 
+PRECONDITION_S = 0.08  # bench.py's power-transient preconditioning
+
+
 def time_kernel(fn, stream, reps):
+    """Average launch time of fn on `stream`, after untimed launches worth
+    PRECONDITION_S of GPU time (the first ~30-60 ms of back-to-back launches
+    after idle run slow while the SMU settles the clocks, bench.py)."""
     fn()
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < PRECONDITION_S:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record(stream)
     for _ in range(reps):

@@ -19,6 +19,13 @@ from bench_extra import dev, time_kernel  # noqa: E402
 
 SHAPES = [  # name, start offset in slot, length, slot stride
     ("aligned 4096", 0, 4096, 4096),
+    ("aligned 4080 (f 255, no tail; window at -16)", 0, 4080, 4096),
+    ("aligned 4064 (window at -32)", 0, 4064, 4096),
+    ("aligned 4032 (window at -64)", 0, 4032, 4096),
+    ("aligned 3968 (window at -128)", 0, 3968, 4096),
+    ("head 64, 4032 (window at 0)", 64, 4032, 4096),
+    ("aligned 4092 (f 255, tail 12)", 0, 4092, 4096),
+    ("head 16, 4080 (f 255 at +16)", 16, 4080, 4096),
     ("head 3, 4093 (f 256, no tail)", 3, 4093, 4096),
     ("aligned 4099 (tail 3)", 0, 4099, 4112),
     ("head 3, 4096 (tail 3)", 3, 4096, 4112),
@@ -29,6 +36,7 @@ SHAPES = [  # name, start offset in slot, length, slot stride
 
 
 def main():
+    only = sys.argv[1] if len(sys.argv) > 1 else ""
     d = torch.device("cuda", 0)
     st = torch.cuda.current_stream(d)
     n = 1 << 20
@@ -38,6 +46,8 @@ def main():
         eng.fill_splitmix64_device(buf, 5, stream=st.cuda_stream)
         host = None
         for name, h, ln, stride in SHAPES:
+            if only and only not in name:
+                continue
             offs = (np.arange(n, dtype=np.uint64) * stride + h).astype(np.uint64)
             lens = np.full(n, ln, np.uint32)
             do, dl = dev(offs, d), dev(lens, d)

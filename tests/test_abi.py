@@ -78,3 +78,17 @@ def test_cpp_surface_drop_in_cpu(tmp_path):
     r = subprocess.run([exe, "0"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
+
+
+def test_kernel_span_geometry_host(tmp_path):
+    """tests/cpp/test_walk.cc: the LDS kernels' span geometry
+    (wipdb_amd/csrc/crc32c_walk.h) on the host -- every DMA source of every
+    span shape stays in the span's pages, and replaying the kernel's
+    arithmetic on those sources gives Extend() and ReadBlock's verdict for
+    84 k (start, length, init, verify) cases."""
+    exe = str(tmp_path / "test_walk")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "wipdb_amd", "csrc"),
+                    os.path.join(REPO, "tests", "cpp", "test_walk.cc"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "PASS" in r.stdout

@@ -44,7 +44,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "crc32c_lds.h"
+#include "crc32c_walk.h"
 
 namespace wipdb {
 namespace lk {
@@ -87,6 +90,7 @@ struct Lane {
   uint32_t km;      // byte j: 32 t_j + 4 (l & 7)               (main tables)
   uint32_t k1;      // byte j: 128 + 4 (4 a + t_j), a = 7 - l % 8 (fold level 1)
   uint32_t k2;      // byte j: 8 (4 c + t_j), c = 7 - l / 8     (fold level 2, >> 1)
+  uint32_t k1b;     // byte j: 128 + 4 (4 b + t_j), b = 3 - l % 4 (4-lane groups' level 1)
 };
 
 // G: spans per wave (groups of 64 / G lanes); the level-2 fold shifts the
@@ -97,7 +101,7 @@ __device__ __forceinline__ Lane make_lane(uint32_t l) {
   constexpr uint32_t LG = 64u / G;
   const uint32_t q = (l >> 3) & 3u, r = l & 7u, a = 7u - (l & 7u);
   const uint32_t c = (LG / 8u - 1u) - ((l % LG) >> 3);
-  k.km = k.k1 = k.k2 = 0;
+  k.km = k.k1 = k.k2 = k.k1b = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
     const uint32_t t = (j + q) & 3u;
@@ -105,6 +109,7 @@ __device__ __forceinline__ Lane make_lane(uint32_t l) {
     k.km |= (t * 32u + r * 4u) << (8 * j);
     k.k1 |= (128u + (a * 4u + t) * 4u) << (8 * j);
     k.k2 |= (8u * (c * 4u + t)) << (8 * j);
+    k.k1b |= (128u + ((3u - (l & 3u)) * 4u + t) * 4u) << (8 * j);
   }
   return k;
 }
@@ -295,6 +300,9 @@ __device__ __forceinline__ void dma2(uint64_t base, uint32_t slot, uint32_t o0, 
 
 __device__ __forceinline__ void dma1nt(uint64_t base, uint32_t dst, uint32_t off) {
   uint32_t keep;
+  // (callers' values are uniform; say so, so they stay in SGPRs under a lane branch)
+  dst = __builtin_amdgcn_readfirstlane(dst);
+  base = uni64(base);
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
@@ -303,6 +311,21 @@ __device__ __forceinline__ void dma1nt(uint64_t base, uint32_t dst, uint32_t off
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(off), "s"(dst), "s"(base)
+      : "memory");
+}
+
+// One DMA with per-lane 64-bit source addresses (the lanes of one
+// instruction may serve different spans).
+__device__ __forceinline__ void dma1v(uint64_t addr, uint32_t dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(addr), "s"(dst)
       : "memory");
 }
 
@@ -329,14 +352,6 @@ __device__ __forceinline__ void load_image(const uint8_t* image, uint32_t w, uin
 // arguments, so the compiler loads them with SMEM (asynchronously, waited
 // for at first use).
 // ---------------------------------------------------------------------------
-struct SpanD {
-  uint64_t a;      // offset of the first byte from the source base
-  uint32_t n;      // bytes
-  uint32_t init;   // Extend's init_crc
-  uint32_t link;   // class-1 list entry cut after its first segment: kLinkValid | remainder
-  uint64_t id;     // output slot
-};
-constexpr uint32_t kLinkValid = 0x40000000u;  // SpanD.link: the span is cut (link in low bits)
 
 // Descriptor batch: span i = base + offsets[i], lengths[i] (+ extra) bytes.
 struct DescSrc {
@@ -381,12 +396,9 @@ struct ListSrc {
 // ---------------------------------------------------------------------------
 // Segments of a span (uniform).
 // ---------------------------------------------------------------------------
+// (the size-class list kernels' segments: a chunk grid that starts at the
+// span's first 16-byte-aligned chunk, with a ragged tail)
 constexpr uint32_t kSegValid = 1u, kSegFirst = 2u, kSegLast = 4u, kSegCut = 8u;
-// kSegPiece: the span's last segment; its remainder (at most kPieceChunks
-// chunks + the tail) joins the wave's piece ring.  kSegBatch: not a segment
-// but a batch of up to 8 pieces (nc pieces from ring entry init).
-constexpr uint32_t kSegPiece = 16u, kSegBatch = 32u;
-constexpr uint32_t kPieceChunks = 32;
 
 struct Seg {
   uint64_t a0;    // offset of the segment's first chunk (16-byte aligned address)
@@ -396,7 +408,6 @@ struct Seg {
   uint32_t flags;
   uint32_t init;  // first segment: the span's init
   uint32_t link;  // cut: where its partial CRC goes
-  uint32_t pw;    // kSegPiece: the piece's chunks | tail bytes << 8
   uint64_t id;    // output slot
 };
 
@@ -417,12 +428,9 @@ struct Geo {
 struct Walk {
   uint64_t a0, id;
   uint32_t f, h, t, init, k, nseg, link;
-  bool cut, piece, valid;
+  bool cut, valid;
 
-  // pieces: a span of more than 256 chunks whose last 1..kPieceChunks chunks
-  // (+ tail) would need a whole segment iteration leaves them to the piece
-  // ring instead
-  __device__ __forceinline__ void start(const uint8_t* base, const SpanD& d, bool pieces = false) {
+  __device__ __forceinline__ void start(const uint8_t* base, const SpanD& d) {
     const Geo g(reinterpret_cast<uint64_t>(base) + d.a, d.n);
     h = g.h;
     f = g.f;
@@ -433,9 +441,7 @@ struct Walk {
     link = d.link;
     k = 0;
     cut = (d.link & kLinkValid) != 0u;
-    const uint32_t r = f % kSegChunks;
-    piece = pieces && !cut && f > kSegChunks && r != 0u && r <= kPieceChunks;
-    nseg = cut ? 1u : (piece ? f / kSegChunks : (f == 0u ? 1u : (f + kSegChunks - 1u) / kSegChunks));
+    nseg = cut ? 1u : (f == 0u ? 1u : (f + kSegChunks - 1u) / kSegChunks);
     valid = true;
   }
   __device__ __forceinline__ Seg next() {
@@ -448,12 +454,10 @@ struct Walk {
     // the tail: bytes [0, t) of the chunk after the last full one; a span
     // inside one chunk (f == 0) is all tail, bytes [h, t)
     g.o = f == 0u ? h : 0u;
-    g.e = (last && !cut && !piece) ? t : 0u;
-    g.flags = kSegValid | (k == 0u ? kSegFirst : 0u) | (last ? kSegLast : 0u) | (cut ? kSegCut : 0u) |
-              (last && piece ? kSegPiece : 0u);
+    g.e = (last && !cut) ? t : 0u;
+    g.flags = kSegValid | (k == 0u ? kSegFirst : 0u) | (last ? kSegLast : 0u) | (cut ? kSegCut : 0u);
     g.init = init;
     g.link = link;
-    g.pw = piece ? (f % kSegChunks) | (t << 8) : 0u;
     g.id = id;
     if (last) valid = false;
     ++k;
@@ -468,9 +472,6 @@ __device__ __forceinline__ uint32_t head_register(uint32_t l, uint32_t init, uin
 }
 
 // Byte mask of word ww of a chunk whose first h bytes are not the span's.
-__device__ __forceinline__ uint32_t head_mask(uint32_t h, uint32_t ww) {
-  return h >= 4u * ww + 4u ? 0u : (h <= 4u * ww ? ~0u : (~0u << (8u * (h - 4u * ww))));
-}
 
 // LE32 at byte e (< 16) of the 32 bytes lo || hi (a verify trailer).
 __device__ __forceinline__ uint32_t le32_at(const u32x4& lo, const u32x4& hi, uint32_t e) {
@@ -706,23 +707,74 @@ __device__ __forceinline__ void run1(const Src& src, void* out, uint32_t flags, 
   }
 }
 
-// ---------------------------------------------------------------------------
-// The descriptor / strided / verify pipeline: G = 1 segments, plus pieces.
-// A span of more than 256 chunks whose last 1..32 chunks (+ tail) would cost
-// a whole 64-lane segment iteration (a table block: 4 KiB + its last entry +
-// the type byte) hands them, with the register after its last full segment,
-// to the wave's piece ring: entry k in lane k of five VGPRs.  Once 8 are
-// pending (or the wave runs out of segments), one iteration CRCs them all,
-// a piece per 8-lane group (a 32-chunk window each, two per DMA instruction
-// of half a wave), folded within the group (level 1 + DPP: no level 2).
-// ---------------------------------------------------------------------------
-// The fold of 8-lane groups: valid in each group's lane 8g.
-__device__ __forceinline__ uint32_t fold8(const Lane& k, uint32_t l, uint32_t r) {
-  uint32_t v = fold_l1(k, l, r);
-  v ^= dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v ^= dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-  v ^= dpp<0x104>(v);  // row_shl:4 -> lanes 8k hold their block of 8
+// The descriptor / strided / verify pipeline: the END-ALIGNED GRID
+// (crc32c_walk.h: the grid, segments, pieces and their DMA sources).
+// Main path: zero the window chunks in front of the segment (front, uniform)
+// and put chunk 0 (window index front: lane front / 4, chunk front % 4) in
+// its span form.
+__device__ __forceinline__ void prepare_first(uint32_t (&W)[16], uint32_t l, uint32_t front,
+                                              uint32_t hp, uint32_t ws, uint32_t inj) {
+  if (front != 0u) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool z = static_cast<int32_t>(4u * l) + i < static_cast<int32_t>(front);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) W[4 * i + w] = z ? 0u : W[4 * i + w];
+    }
+  }
+  const bool me = l == (front >> 2);
+  // the chunk index is uniform: one static case
+  auto apply = [&](auto I) {
+    constexpr int i = decltype(I)::value;
+    uint32_t c[4] = {W[4 * i], W[4 * i + 1], W[4 * i + 2], W[4 * i + 3]};
+    fix_head(c, hp, ws, inj);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) W[4 * i + w] = me ? c[w] : W[4 * i + w];
+  };
+  switch (front & 3u) {
+    case 0: apply(std::integral_constant<int, 0>()); break;
+    case 1: apply(std::integral_constant<int, 1>()); break;
+    case 2: apply(std::integral_constant<int, 2>()); break;
+    default: apply(std::integral_constant<int, 3>()); break;
+  }
+}
+
+// Feeds the k (<= 3) low bytes of word tw into register r in one slicing
+// step (tw = 0: r * x^(8k)).  Per lane.
+__device__ __forceinline__ uint32_t tail_step(const Lane& lk, uint32_t r, uint32_t tw, uint32_t k) {
+  const uint32_t x = (r ^ tw) << (8u * (4u - (k == 0u ? 4u : k)) & 31u);
+  const uint32_t v = step(lk, k == 0u ? 0u : x, 0u) ^ (k == 0u ? r : (r >> (8u * k)));
   return v;
+}
+
+// The fold of 4-lane groups: lane l's register shifted by 64 (3 - l % 4)
+// bytes (level-1 tables), XOR over the quad.  Valid in every lane.
+__device__ __forceinline__ uint32_t fold4(const Lane& k, uint32_t l, uint32_t r) {
+  const uint32_t a0 = lds_ld(kLdsMain + __builtin_amdgcn_perm(k.k1b, r, k.sel[0]));
+  const uint32_t a1 = lds_ld(kLdsMain + __builtin_amdgcn_perm(k.k1b, r, k.sel[1]));
+  const uint32_t a2 = lds_ld(kLdsMain + __builtin_amdgcn_perm(k.k1b, r, k.sel[2]));
+  const uint32_t a3 = lds_ld(kLdsMain + __builtin_amdgcn_perm(k.k1b, r, k.sel[3]));
+  uint32_t v = (l & 3u) == 3u ? r : (xor3(a0, a1, a2) ^ a3);
+  v ^= dpp<0xB1>(v);  // quad_perm [1,0,3,2]
+  v ^= dpp<0x4E>(v);  // quad_perm [2,3,0,1]
+  return v;
+}
+
+// r * x^(8 * 512 c) mod P from the level-2 tables, for any lane (kc: the
+// lane's selector constant for column c, make_l2c).
+__device__ __forceinline__ uint32_t l2_shift(const Lane& k, uint32_t kc, uint32_t r) {
+  const uint32_t a0 = lds_ld(kLdsL2 + (__builtin_amdgcn_perm(kc, r, k.sel[0]) >> 1));
+  const uint32_t a1 = lds_ld(kLdsL2 + (__builtin_amdgcn_perm(kc, r, k.sel[1]) >> 1));
+  const uint32_t a2 = lds_ld(kLdsL2 + (__builtin_amdgcn_perm(kc, r, k.sel[2]) >> 1));
+  const uint32_t a3 = lds_ld(kLdsL2 + (__builtin_amdgcn_perm(kc, r, k.sel[3]) >> 1));
+  return xor3(a0, a1, a2) ^ a3;
+}
+__device__ __forceinline__ uint32_t make_l2c(uint32_t l, uint32_t c) {
+  const uint32_t q = (l >> 3) & 3u;
+  uint32_t kc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) kc |= (8u * (c * 4u + ((j + q) & 3u))) << (8 * j);
+  return kc;
 }
 
 __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t lane) {
@@ -731,23 +783,24 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t lane) {
 }
 
 struct PieceRing {
-  uint32_t a_lo, a_hi, pw, R, id;  // per lane: entry `lane`
-  uint32_t head, count;            // uniform
-  __device__ __forceinline__ void push(uint32_t l, uint64_t a0, uint32_t w, uint32_t reg,
-                                       uint32_t sid) {
+  uint32_t a_lo, a_hi, pw, inj, T, id;  // per lane: entry `lane`
+  uint32_t head, count;                 // uniform
+  __device__ __forceinline__ void push(uint32_t l, uint64_t c0, uint32_t w, uint32_t reg,
+                                       uint32_t t, uint32_t sid) {
     const bool me = l == ((head + count) & 63u);
-    a_lo = me ? static_cast<uint32_t>(a0) : a_lo;
-    a_hi = me ? static_cast<uint32_t>(a0 >> 32) : a_hi;
+    a_lo = me ? static_cast<uint32_t>(c0) : a_lo;
+    a_hi = me ? static_cast<uint32_t>(c0 >> 32) : a_hi;
     pw = me ? w : pw;
-    R = me ? reg : R;
+    inj = me ? reg : inj;
+    T = me ? t : T;
     id = me ? sid : id;
     ++count;
   }
 };
 
 template <int OUT, typename Src>
-__device__ __forceinline__ void run_p(const Src& src, void* out, uint32_t flags,
-                                      const uint8_t* image) {
+__device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags,
+                                       const uint8_t* image) {
   const uint32_t l = threadIdx.x & 63u;
   const uint32_t w = uni(threadIdx.x >> 6);
   const uint64_t count = src.count;
@@ -758,6 +811,7 @@ __device__ __forceinline__ void run_p(const Src& src, void* out, uint32_t flags,
   pp.init(l, w);
   const bool msk = (flags & kFlagMask) != 0u;
   const uint64_t sbase = reinterpret_cast<uint64_t>(src.base);
+  constexpr bool kVerify = OUT == 1;
 
   struct Pref {
     SpanD d;
@@ -768,40 +822,48 @@ __device__ __forceinline__ void run_p(const Src& src, void* out, uint32_t flags,
     p.valid = s < count;
     if (p.valid) p.d = src.get(s);
   };
-  auto issue = [&](const Seg& g) {
-    if (g.nc != 0u) pp.issue<4>(sbase + g.a0, 0u, kSegChunks, g.nc);
-    if ((g.flags & (kSegLast | kSegPiece)) == kSegLast)
-      pp.issue_end(sbase + g.a0 + 16u * g.nc, 0u, g.e > g.o, OUT == 1, g.e);
+  auto issue = [&](const SegE& g) {
+    if (!(g.c.flags() & kENoBody)) {
+      const uint64_t b = sbase + g.wb;
+      const uint32_t o = 16u * pp.cm;
+      if (g.src0 == 0u)
+        dma4(b, pp.slot, o, o + 1024u, o + 2048u, o + 3072u);
+      else
+        dma4(b, pp.slot, SegChunkOffset(g, pp.cm), SegChunkOffset(g, pp.cm + 64u),
+             SegChunkOffset(g, pp.cm + 128u), SegChunkOffset(g, pp.cm + 192u));
+    }
+    if (g.c.flags() & kEAux) dma_piece(l, sbase + g.ax, 0u, AuxAddr(w, kAuxTail));
   };
-  PieceRing ring{0, 0, 0, 0, 0, 0, 0};
-  // a batch of the ring's next n (<= 8) pieces: its DMAs
+  PieceRing ring{0, 0, 0, 0, 0, 0, 0, 0};
+  // a batch of the ring's next n (<= 16) pieces: their DMAs (16-chunk
+  // windows END-aligned at each piece's last chunk).  Instruction q loads
+  // pieces 4q .. 4q + 3, a quarter wave each, into slot KiB q: piece p's
+  // window is slot bytes [256 p, 256 p + 256).
   auto issue_batch = [&](uint32_t h0, uint32_t n) {
 #pragma unroll
-    for (uint32_t g = 0; g < 8; ++g) {
-      if (g >= n) break;
-      const uint32_t idx = (h0 + g) & 63u;
-      const uint64_t a0 = (static_cast<uint64_t>(uni(__builtin_amdgcn_readlane(ring.a_hi, idx))) << 32) |
-                          uni(__builtin_amdgcn_readlane(ring.a_lo, idx));
-      const uint32_t pw = uni(__builtin_amdgcn_readlane(ring.pw, idx));
-      const uint32_t nc = pw & 63u, e = (pw >> 8) & 15u;
-      const uint64_t base = sbase + a0;
-      if ((l >> 5) == (g & 1u)) {
-        // window chunk (cm mod 32) of the group is piece chunk (cm mod 32) - (32 - nc)
-        const int32_t b = 16 * (static_cast<int32_t>(pp.cm & 31u) - static_cast<int32_t>(32u - nc));
-        dma1nt(base, pp.slot + 1024u * (g >> 1), static_cast<uint32_t>(max(b, 0)));
-      }
-      pp.issue_end(base + 16u * nc, g, e != 0u, OUT == 1, e);
+    for (uint32_t q = 0; q < 4; ++q) {
+      if (4u * q >= n) break;
+      const uint32_t p = 4u * q + (l >> 4);
+      const uint32_t idx = (h0 + p) & 63u;
+      const uint64_t c0 = (static_cast<uint64_t>(bperm(ring.a_hi, idx)) << 32) | bperm(ring.a_lo, idx);
+      const uint32_t pw = bperm(ring.pw, idx);
+      // lane m of the quarter loads window chunk cm mod 16 of its piece
+      if (p < n) dma1v(sbase + c0 + PieceChunkOffset(pw, pp.cm & 15u), pp.slot + 1024u * q);
     }
   };
 
-  Walk wk;
+  WalkE wk;
   Pref pf;
   prefetch(pf);
   if (!pf.valid) return;
-  wk.start(src.base, pf.d, true);
+  wk.start(sbase, pf.d, kVerify);
   prefetch(pf);
-  Seg cur = wk.next();
-  issue(cur);
+  SegC cur;
+  {
+    const SegE g = wk.next(kVerify);
+    issue(g);
+    cur = g.c;
+  }
   uint32_t chain = 0;  // register carried between the segments of a span
   bool stored_prev = false;
   g_u32* const out32 = (g_u32*)(reinterpret_cast<uintptr_t>(out));
@@ -812,94 +874,103 @@ __device__ __forceinline__ void run_p(const Src& src, void* out, uint32_t flags,
     else wait_vm<0>();
     uint32_t W[16];
     pp.read(W);
-    // this lane's group's aux pieces (a segment: group 0)
-    const uint32_t grp = (cur.flags & kSegBatch) ? l >> 3 : 0u;
-    const u32x4 tl = pp.piece_lane(kAuxTail + grp);
-    const u32x4 nx = OUT == 1 ? pp.piece_lane(kAuxNext + grp) : u32x4{0, 0, 0, 0};
+    u32x4 ax{0, 0, 0, 0};
+    if (cur.flags() & kEAux) ax = pp.piece(kAuxTail);
     pp.release();
     // the next iteration: a batch of 8 pieces, the rest of this span, or
     // the prefetched span
-    Seg nxt;
-    nxt.flags = 0;
+    SegC nxt;
+    nxt.g1 = 0;
     bool took_pf = false;
     const bool more = wk.valid || pf.valid;
-    if (ring.count >= 8u || (ring.count != 0u && !more)) {
-      const uint32_t n = ring.count < 8u ? ring.count : 8u;
-      nxt.flags = kSegValid | kSegBatch;
+    if (ring.count >= kBatch || (ring.count != 0u && !more)) {
+      const uint32_t n = ring.count < kBatch ? ring.count : kBatch;
+      nxt.g1 = kEValid | kEBatch;
       nxt.init = ring.head;
-      nxt.nc = n;
+      nxt.id = n;
       issue_batch(ring.head, n);
       ring.head = (ring.head + n) & 63u;
       ring.count -= n;
     } else if (more) {
       if (!wk.valid) {
-        wk.start(src.base, pf.d, true);
+        wk.start(sbase, pf.d, kVerify);
         took_pf = true;
       }
-      nxt = wk.next();
-      issue(nxt);
+      const SegE g = wk.next(kVerify);
+      issue(g);
+      nxt = g.c;
     }
 
     bool did_store = false;
-    if (cur.flags & kSegBatch) {
-      // ---- a batch of pieces, one per 8-lane group ----
-      const uint32_t g = l >> 3, gl = l & 7u;
+    if (cur.flags() & kEBatch) {
+      // ---- a batch of front pieces, one per 4-lane group ----
+      const uint32_t g = l >> 2, gl = l & 3u;
       const uint32_t idx = (cur.init + g) & 63u;
-      const bool on = g < cur.nc;
-      const uint32_t pw = bperm(ring.pw, idx), reg = bperm(ring.R, idx);
-      const uint32_t nc = on ? pw & 63u : 0u, e = on ? (pw >> 8) & 15u : 0u;
+      const bool on = g < cur.id;
+      const uint32_t pw = bperm(ring.pw, idx), inj = bperm(ring.inj, idx);
+      const uint32_t T = bperm(ring.T, idx), sid = bperm(ring.id, idx);
+      const int32_t front = static_cast<int32_t>(kPieceChunks - (on ? pw & 63u : 0u));
+      const uint32_t hp = (pw >> 8) & 15u, ws = (pw >> 12) & 3u, k = (pw >> 14) & 3u;
+      // zero the chunks in front of the piece; its chunk 0 into span form
+      uint32_t c[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int32_t c = static_cast<int32_t>(4u * gl) + i - static_cast<int32_t>(32u - nc);
+        const int32_t ci = static_cast<int32_t>(4u * gl) + i - front;
 #pragma unroll
-        for (uint32_t ww = 0; ww < 4; ++ww) W[4 * i + ww] &= c < 0 ? 0u : ~0u;
-        W[4 * i] ^= c == 0 ? reg : 0u;
+        for (int q = 0; q < 4; ++q) {
+          c[q] = ci == 0 ? W[4 * i + q] : c[q];
+          W[4 * i + q] = ci < 0 ? 0u : W[4 * i + q];
+        }
       }
-      uint32_t r = fold8(lk, l, scan(lk, W));
-      r = feed_tail_lanes(lk, l, r, tl, 0u, gl == 0u ? e : 0u);
-      const uint32_t crc = ~r;
-      const uint32_t sid = bperm(ring.id, idx);
+      fix_head(c, hp, ws, inj);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool h0 = static_cast<int32_t>(4u * gl) + i - front == 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) W[4 * i + q] = h0 ? c[q] : W[4 * i + q];
+      }
+      const uint32_t rp = fold4(lk, l, scan(lk, W));
       if (gl == 0u && on) {
-        if (OUT == 1) out8[sid] = unmask_crc(le32_at(tl, nx, e)) == crc ? 1u : 0u;
-        else out32[sid] = msk ? mask_crc(crc) : crc;
+        // register of the whole span = rp * x^(8 (4096 + k)) ^ main register
+        const uint32_t sft = l2_shift(lk, make_l2c(l, 1u), l2_shift(lk, make_l2c(l, 7u), rp));
+        const uint32_t v = tail_step(lk, sft, 0u, k) ^ T;
+        if (kVerify) out8[sid] = v == 0u ? 1u : 0u;
+        else out32[sid] = msk ? mask_crc(~v) : ~v;
       }
       did_store = true;
     } else {
       // ---- CRC of the current segment ----
+      const uint32_t fl = cur.flags();
       uint32_t R;
-      if (cur.nc == 0u) {
-        R = ~cur.init;  // a span inside one chunk: all of it is tail
+      if (fl & kENoBody) {
+        R = ~cur.init;
       } else {
-        const uint32_t inj = (cur.flags & kSegFirst) ? head_register(l, cur.init, cur.h) : chain;
-        if (cur.nc == kSegChunks && cur.h == 0u) {
+        const uint32_t inj = (fl & kEFirst) ? head_register(l, cur.init, cur.hp())
+                                            : ((fl & kEMain) ? 0u : chain);
+        if ((cur.g1 & 0x1fff00u) == 0u) {  // front == 0, hp == 0
           W[0] ^= l == 0u ? inj : 0u;
         } else {
-          // chunk i of lane l is segment chunk 4l + i - (256 - nc): zero the
-          // ones in front of the segment, mask the first h bytes of chunk 0
-          // and put the register there
-          const int32_t base = static_cast<int32_t>(kSegChunks - cur.nc);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int32_t ci = static_cast<int32_t>(4u * l) + i - base;
-#pragma unroll
-            for (uint32_t ww = 0; ww < 4; ++ww)
-              W[4 * i + ww] &= ci < 0 ? 0u : (ci == 0 ? head_mask(cur.h, ww) : ~0u);
-            W[4 * i] ^= ci == 0 ? inj : 0u;
-          }
+          prepare_first(W, l, cur.front(), cur.hp(), cur.ws(), inj);
         }
         R = fold<1>(lk, l, scan(lk, W))[0];
       }
-      if (cur.flags & kSegPiece) {
-        // the rest goes to the ring, continuing from R
-        ring.push(l, cur.a0 + kSegChunks * 16u, cur.pw, R, static_cast<uint32_t>(cur.id));
-      } else if (cur.flags & kSegLast) {
-        const u32x4 t{uni(tl.x), uni(tl.y), uni(tl.z), uni(tl.w)};
-        if (cur.e > cur.o) R = feed_tail(lk, l, R, t, cur.o, cur.e);
-        const uint32_t crc = ~R;
+      uint32_t stored_x = 0;  // verify: ~Unmask(the stored crc)
+      if (fl & kEAux) {
+        const u32x4 a{uni(ax.x), uni(ax.y), uni(ax.z), uni(ax.w)};
+        if (cur.k() != 0u) R = uni(tail_step(lk, R, le32_at(a, u32x4{0, 0, 0, 0}, cur.te()), cur.k()));
+        if (kVerify) stored_x = ~unmask_crc(le32_at(a, u32x4{0, 0, 0, 0}, cur.tv()));
+      }
+      if (fl & kEMain) {
+        // the front piece goes to the ring with its head register; the span
+        // is finished there: rp * x^(8 (4096 + k)) ^ T (== 0 <=> a good block)
+        const uint32_t pw = cur.piece_word();
+        const uint32_t hin = head_register(l, cur.init, cur.php());
+        ring.push(l, cur.c0, pw, hin, kVerify ? R ^ stored_x : R, cur.id);
+      } else if (fl & kELast) {
         did_store = true;
         if (l == 0u) {
-          if (OUT == 1) out8[cur.id] = unmask_crc(le32_at(t, nx, cur.e)) == crc ? 1u : 0u;
-          else out32[cur.id] = msk ? mask_crc(crc) : crc;
+          if (kVerify) out8[cur.id] = R == stored_x ? 1u : 0u;
+          else out32[cur.id] = msk ? mask_crc(~R) : ~R;
         }
       } else {
         chain = R;
@@ -907,14 +978,14 @@ __device__ __forceinline__ void run_p(const Src& src, void* out, uint32_t flags,
     }
     stored_prev = did_store;
 
-    if (!(nxt.flags & kSegValid)) {
+    if (!(nxt.g1 & kEValid)) {
       if (ring.count == 0u) break;
       // the last pieces, pushed by this iteration: their DMAs go out after
       // its store, so the next wait is for everything
       const uint32_t n = ring.count;
-      nxt.flags = kSegValid | kSegBatch;
+      nxt.g1 = kEValid | kEBatch;
       nxt.init = ring.head;
-      nxt.nc = n;
+      nxt.id = n;
       issue_batch(ring.head, n);
       ring.head = (ring.head + n) & 63u;
       ring.count = 0;
@@ -1131,7 +1202,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const DescSrc src{base, offsets, lengths, inits, count, 0u};
-  run_p<0>(src, out, flags, image);
+  run_ea<0>(src, out, flags, image);
 }
 
 // Fixed-size blocks at a fixed stride.
@@ -1139,7 +1210,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t length, uint32_t init,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const StridedSrc src{base, stride, length, init, count};
-  run_p<0>(src, out, flags & kFlagMask, image);
+  run_ea<0>(src, out, flags & kFlagMask, image);
 }
 
 // Read-side verify (ReadBlock, kv/src/table/format.cc:91-99): block i =
@@ -1150,7 +1221,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
     const uint8_t* __restrict__ image) {
   const DescSrc src{base, offsets, lengths, nullptr, count, 1u};
-  run_p<1>(src, status, 0u, image);
+  run_ea<1>(src, status, 0u, image);
 }
 
 // A size-class list (HCRC_SPLIT_SMALL): G = 1 takes the spans of more than

@@ -1,0 +1,229 @@
+// crc32c_walk.h -- the span geometry of the LDS-staged CRC32C kernels
+// (crc32c_lds.hip): the end-aligned chunk grid, its segments and front
+// pieces, and the byte ranges every DMA of a span reads.  Host + device: the
+// kernels use it, and tests/cpp/test_walk.cc runs the same code on the host
+// -- every DMA source of every lane checked against the span's pages, and
+// the kernel's arithmetic replayed with a byte-serial CRC -- so a geometry
+// change is checked before it reaches a GPU.  DESIGN.md section 4.
+#pragma once
+#include <stdint.h>
+
+#include "crc32c_lds.h"
+
+namespace wipdb {
+namespace lk {
+
+// A span as a source hands it out (all values uniform).
+struct SpanD {
+  uint64_t a;      // offset of the first byte from the source base
+  uint32_t n;      // bytes
+  uint32_t init;   // Extend's init_crc
+  uint32_t link;   // class-1 list entry cut after its first segment: kLinkValid | remainder
+  uint64_t id;     // output slot
+};
+constexpr uint32_t kLinkValid = 0x40000000u;  // SpanD.link: the span is cut (link in low bits)
+
+// Byte mask of word ww of chunk 0: its first h bytes are not the span's.
+WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {
+  return h >= 4u * ww + 4u ? 0u : (h <= 4u * ww ? ~0u : (~0u << (8u * (h - 4u * ww))));
+}
+
+// ---------------------------------------------------------------------------
+// The descriptor / strided / verify pipeline: the END-ALIGNED GRID.
+//
+// A span of n bytes at s ends at E = s + n; E4 = E rounded down to a 4-byte
+// boundary (of the address).  The k = E - E4 <= 3 trailing bytes are the
+// span's tail; the body [s, E4) is cut into C = ceil((E4 - s) / 16) chunks
+// whose grid ENDS at E4: chunk j = [E4 - 16 (C - j), +16), so every chunk
+// starts on a 4-byte boundary (global_load_lds_dwordx4 at dword alignment
+// costs ~2 % over 16-byte alignment; at byte alignment 30-40 %,
+// scripts/probes/dma_align_probe.hip, scripts/probe_shapes.py) and only
+// chunk 0 is partial: hp = 16 C - (E4 - s) of its leading bytes are not the
+// span's and are masked -- or, when reading them could cross into the page
+// below s, chunk 0 is read from s rounded down to 4 and shifted right by whole
+// words before the mask.  The tail is ONE slicing step:
+//   reg' = T-step((reg ^ tail word) << 8 (4 - k)) ^ (reg >> 8 k),
+// with the tail word (and a verify span's stored trailer) in 16 bytes read
+// with the last segment.  Nothing outside [s, E) (+ the 4 trailer bytes of a
+// verify span) is read, except within the 4-byte words holding s and E.
+//
+// Segments are 256-chunk windows END-aligned at their last chunk: the first
+// covers chunks [0, C - 256 (m - 1)), the m - 1 others 256 each, chained by
+// the register.  A span of 257..288 chunks (a table block: 4 KiB + its last
+// entry + the type byte) is instead ONE full main segment -- its last 256
+// chunks and its tail, from a zero register -- plus a front piece of its first
+// 1..16 chunks, which joins the wave's piece ring: entry k in lane k of six
+// VGPRs.  Once 16 are pending (or the wave runs out of segments), one
+// iteration CRCs them all, a piece per 4-lane group (a 16-chunk window each,
+// four per DMA instruction with per-lane addresses), folded within the group
+// (level 1 + DPP), and finishes each span by linearity:
+//   register = piece register * x^(8 (4096 + k)) ^ main register.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kEValid = 1u, kEFirst = 2u, kELast = 4u, kEMain = 8u, kEBatch = 16u,
+                   kENoBody = 32u, kEAux = 64u;
+constexpr uint32_t kPieceChunks = 16;  // a piece: 4 lanes x 4 chunks
+constexpr uint32_t kBatch = 16;        // pieces per batch iteration
+
+// A segment as issued (DMA sources) and as computed (the packed SegC, the
+// only part kept live across the iteration: SGPRs are the kernel's scarce
+// resource).
+//   g1: flags (8) | front (9) << 8 | hp (4) << 17 | ws (2) << 21 | k (2) << 23 |
+//       te (4) << 25
+//   g2: tv (4) | main: the front piece's chunks (5) << 4 | its hp (4) << 9 |
+//       its ws (2) << 13
+struct SegC {
+  uint32_t g1, g2;
+  uint32_t init;  // first segment / main: the span's init (batch: ring head)
+  uint32_t id;    // output slot (batch: the number of pieces)
+  uint64_t c0;    // main: offset of the span's chunk 0 (the piece's)
+  WIPDB_LK_HD inline uint32_t flags() const { return g1 & 0xffu; }
+  WIPDB_LK_HD inline uint32_t front() const { return (g1 >> 8) & 0x1ffu; }
+  WIPDB_LK_HD inline uint32_t hp() const { return (g1 >> 17) & 15u; }
+  WIPDB_LK_HD inline uint32_t ws() const { return (g1 >> 21) & 3u; }
+  WIPDB_LK_HD inline uint32_t k() const { return (g1 >> 23) & 3u; }
+  WIPDB_LK_HD inline uint32_t te() const { return (g1 >> 25) & 15u; }
+  WIPDB_LK_HD inline uint32_t tv() const { return g2 & 15u; }
+  WIPDB_LK_HD inline uint32_t r() const { return (g2 >> 4) & 31u; }
+  WIPDB_LK_HD inline uint32_t php() const { return (g2 >> 9) & 15u; }
+  WIPDB_LK_HD inline uint32_t pws() const { return (g2 >> 13) & 3u; }
+  // the ring word of a main segment's front piece
+  WIPDB_LK_HD inline uint32_t piece_word() const { return r() | (php() << 8) | (pws() << 12) | (k() << 14); }
+};
+struct SegE {
+  SegC c;
+  uint64_t wb;    // offset (from the source base) of window chunk 0
+  uint64_t ax;    // last: offset of the 16 bytes holding the tail word / verify trailer
+  uint32_t src0;  // DMA offset (from wb) of the span's chunk 0, also read by the in-front lanes
+};
+
+struct WalkE {
+  uint64_t c0, ax;
+  uint32_t id, init;
+  uint32_t geo;   // hp | ws << 4 | k << 6 | te << 8 | tv << 12 | piece << 16
+  uint32_t nc0;   // chunks of the first segment (piece: the piece's)
+  uint32_t j, nseg;
+  bool valid;
+
+  // sbase: the source base address; verify: the span is followed by a
+  // 4-byte trailer that the last segment reads.  Scalar work per span is the
+  // kernels' scarce resource (one scalar unit per CU serves 16 waves): the
+  // rare parts -- the aux chunk, a head read late, pieces, several segments
+  // -- sit behind uniform branches.
+  WIPDB_LK_HD inline void start(uint64_t sbase, const SpanD& d, bool verify) {
+    const uint32_t n = d.n;
+    const uint32_t s_lo = static_cast<uint32_t>(sbase) + static_cast<uint32_t>(d.a);
+    const uint32_t e_lo = s_lo + n;
+    const uint32_t e3 = e_lo & 3u;
+    const uint32_t k = e3 < n ? e3 : n;  // tail bytes
+    const uint32_t nb = n - k;           // body bytes [s, E4)
+    const uint32_t C = (nb + 15u) >> 4;
+    const uint32_t hp = (C << 4) - nb;
+    c0 = d.a - hp;
+    init = d.init;
+    id = static_cast<uint32_t>(d.id);
+    j = 0;
+    valid = true;
+    geo = hp | (k << 6);
+    const uint32_t pg = s_lo & 4095u;
+    // reading hp bytes in front of s would leave its page: read chunk 0 from
+    // s rounded down to 4, i.e. ws = (hp - s % 4) / 4 words late
+    if (pg < hp) geo |= ((hp - (pg & 3u)) >> 2) << 4;
+    if (C <= kSegChunks) {
+      nseg = 1;
+      nc0 = C;
+      if (C == 0u) geo |= 1u << 17;
+    } else if (C <= kSegChunks + kPieceChunks) {
+      nseg = 1;
+      nc0 = C - kSegChunks;
+      geo |= 1u << 16;
+    } else {
+      nseg = (C + kSegChunks - 1u) / kSegChunks;
+      nc0 = C - kSegChunks * (nseg - 1u);
+    }
+    if (verify || k != 0u) {
+      // the aux chunk: 16 bytes ending at the 4-byte word that holds the
+      // span's last byte (verify: the trailer's last byte) -- or, when they
+      // would start in the page below a short span, from s rounded down to 4
+      const uint32_t need = e_lo + (verify ? 4u : 0u);
+      const uint32_t a_lo = ((need + 3u) & ~3u) - 16u;  // 16 <= n + 7: a_lo may precede s
+      const uint32_t before = s_lo - a_lo;              // bytes in front of s (mod 2^32)
+      const uint32_t a_fix = (before <= 16u && before > pg) ? (s_lo & ~3u) : a_lo;
+      ax = d.a + static_cast<uint64_t>(static_cast<int32_t>(a_fix - s_lo));
+      const uint32_t te = (e_lo - k - a_fix) & 15u;
+      const uint32_t tv = (e_lo - a_fix) & 15u;
+      geo |= (te << 8) | (tv << 12);
+    } else {
+      ax = 0;
+    }
+  }
+  WIPDB_LK_HD inline SegE next(bool verify) {
+    SegE g;
+    const bool last = j + 1u == nseg;
+    const uint32_t hp = geo & 15u, ws = (geo >> 4) & 3u, k = (geo >> 6) & 3u;
+    uint32_t fl = kEValid | (last ? kELast : 0u);
+    if (last && (verify || k != 0u)) fl |= kEAux;
+    g.c.init = init;
+    g.c.id = id;
+    g.c.c0 = c0;
+    g.c.g2 = (geo >> 12) & 15u;
+    g.ax = ax;
+    g.src0 = 0;
+    uint32_t front = 0, h = 0, w = 0;
+    if (geo & (3u << 16)) {
+      if (geo & (1u << 17)) {
+        fl |= kEFirst | kENoBody;
+        g.wb = 0;
+      } else {
+        fl |= kEMain;
+        g.wb = c0 + 16u * nc0;
+        g.c.g2 |= (nc0 << 4) | (hp << 9) | (ws << 13);
+      }
+    } else {
+      // the segment's last chunk, and its window's first
+      g.wb = c0 + 16u * (nc0 + kSegChunks * j) - 16u * kSegChunks;
+      if (j == 0u) {
+        fl |= kEFirst;
+        front = kSegChunks - nc0;
+        h = hp;
+        w = ws;
+        g.src0 = 16u * front + 4u * ws;
+      }
+    }
+    g.c.g1 = fl | (front << 8) | (h << 17) | (w << 21) | (k << 23) | (((geo >> 8) & 15u) << 25);
+    if (last) valid = false;
+    ++j;
+    return g;
+  }
+};
+
+// The DMA source of window chunk t (0..255) of a segment, as a byte offset
+// from sbase + g.wb: the in-front chunks re-read chunk 0's source.
+WIPDB_LK_HD inline uint32_t SegChunkOffset(const SegE& g, uint32_t t) {
+  const uint32_t o = 16u * t;
+  return o > g.src0 ? o : g.src0;
+}
+
+// The DMA source of window chunk t (0..15) of a front piece with ring word
+// pw (chunks | hp << 8 | ws << 12 | k << 14), from sbase + its c0.
+WIPDB_LK_HD inline uint32_t PieceChunkOffset(uint32_t pw, uint32_t t) {
+  const int32_t front = static_cast<int32_t>(kPieceChunks - (pw & 63u));
+  const int32_t s0 = static_cast<int32_t>(4u * ((pw >> 12) & 3u));
+  const int32_t b = 16 * (static_cast<int32_t>(t) - front);
+  return static_cast<uint32_t>(b > s0 ? b : s0);
+}
+
+// Chunk 0 of a span into its span form: read ws words late (shift right by
+// ws words), its hp leading bytes masked, the register inj entering at its
+// first byte.  Per lane.
+WIPDB_LK_HD inline void fix_head(uint32_t (&c)[4], uint32_t hp, uint32_t ws, uint32_t inj) {
+  uint32_t d[4];
+  d[3] = ws == 0u ? c[3] : (ws == 1u ? c[2] : (ws == 2u ? c[1] : c[0]));
+  d[2] = ws == 0u ? c[2] : (ws == 1u ? c[1] : (ws == 2u ? c[0] : 0u));
+  d[1] = ws == 0u ? c[1] : (ws == 1u ? c[0] : 0u);
+  d[0] = ws == 0u ? c[0] : 0u;
+  for (uint32_t w = 0; w < 4; ++w) c[w] = d[w] & head_mask(hp, w);
+  c[0] ^= inj;
+}
+
+}  // namespace lk
+}  // namespace wipdb
