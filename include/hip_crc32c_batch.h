@@ -77,13 +77,10 @@ extern "C" {
 #define HCRC_MASK_OUTPUT 0x2  /* write Mask(crc) instead of crc             */
 /* Size classes: a partition pass sorts the batch into spans of at most
  * ~1 KiB (checksummed 4 per wave iteration), at most ~2 KiB (2 per wave
- * iteration) and longer ones (a wave per 4 KiB segment); a span that just
- * overruns its first 4 KiB segment by up to 2 KiB (a table block: 4096
- * bytes + its last entry + the type byte) is cut there and its remainder
- * continues from the partial CRC in the small classes.  Same results; pays
- * off for batches with many short spans (WAL records, small meta blocks) or
- * table blocks.  hcrc_batch on host memory chooses it by itself.  Uses
- * stream-ordered scratch (~64 bytes per span). */
+ * iteration) and longer ones (the spans kernel's pipeline).  Same results;
+ * pays off for batches with many short spans (WAL records, small meta
+ * blocks).  hcrc_batch on host memory chooses it by itself.  Uses
+ * stream-ordered scratch (~60 bytes per span). */
 #define HCRC_SPLIT_SMALL 0x4
 
 typedef struct hcrc_ctx hcrc_ctx;
@@ -131,9 +128,7 @@ int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base,
                       const uint64_t* d_offsets, const uint32_t* d_lengths,
                       uint8_t* d_status, size_t count, void* stream);
 /* The same with flags: 0 or HCRC_SPLIT_SMALL (the size classes above:
- * small blocks several per wave iteration, a table's data blocks -- 4 KiB
- * plus their last entry -- cut after their first 4 KiB and finished in the
- * small classes). */
+ * small blocks -- meta-index, small filters -- several per wave iteration). */
 int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base,
                          const uint64_t* d_offsets, const uint32_t* d_lengths,
                          uint8_t* d_status, size_t count, int flags, void* stream);
@@ -156,12 +151,13 @@ int hcrc_batch_multi_ex(const int* devices, int ndev, const void* base,
                         const uint32_t* init_crcs, uint32_t* out_crcs,
                         size_t count, int flags, int* shard_rc);
 
-/* Pinned host memory.  hcrc_batch over spans that all lie in ONE range
- * allocated by hcrc_host_alloc or registered by hcrc_host_register (e.g. an
- * mmap'd SST file or a long-lived memtable arena) runs zero-copy: the kernel
- * reads the spans over PCIe directly, with no staging copy.  Anything else
- * (pageable memory, memory pinned by other means, spans spread over several
- * ranges) goes through the pinned staging slots. */
+/* Pinned host memory.  hcrc_batch over spans that each lie inside a range
+ * allocated by hcrc_host_alloc or registered by hcrc_host_register (e.g.
+ * mmap'd SST files, a long-lived memtable arena, a table builder's write
+ * buffers -- one or several ranges) runs zero-copy: the kernel reads the
+ * spans over PCIe directly, with no staging copy.  Anything else (a span in
+ * pageable memory, memory pinned by other means, a span straddling two
+ * ranges) sends the batch through the pinned staging slots. */
 int hcrc_host_alloc(size_t bytes, void** out_ptr);
 int hcrc_host_free(void* ptr);
 int hcrc_host_register(void* ptr, size_t bytes);

@@ -92,6 +92,9 @@ struct TableOptions {
   int device = 0;                    // HIP device for the batched modes
   const Comparator* comparator = nullptr;  // nullptr: BytewiseComparator()
   FilterKeys filter_keys = FilterKeys::kWholeKey;
+  // kBatchGpu / kBatchAuto: the write buffer is pinned host memory (pooled),
+  // so block CRC batches read it zero-copy instead of through staging
+  bool pinned_buffers = true;
 };
 
 // The options WipDB's DB hands its TableBuilders (BuildTableKV,
@@ -173,6 +176,50 @@ Status VerifyTable(const char* image, size_t image_size, int bloom_bits_per_key,
 Status VerifyTables(const char* const* images, const size_t* sizes, size_t n,
                     int bloom_bits_per_key, CrcMode mode, int device,
                     std::vector<Status>* statuses);
+
+// ---- the compaction input path ----
+//
+// VersionSet::MakeInputIteratorKV (kv/src/db/version_set.cc:1348-1373): a
+// merging iterator (table/merger.cc, ties to the lower input) over the input
+// tables' two-level iterators (Table::NewIterator, table.cc:164-229), with
+// ReadOptions::verify_checksums = paranoid_checks.  The reference reads and
+// checks one data block at a time in Table::BlockReader; this reader checks
+// the next `prefetch_blocks` blocks of EVERY input in one CRC batch (on the
+// MI355X in the batched modes) whenever the merge reaches an unchecked
+// block.  Same entries, same order, same status: an input whose Open fails
+// contributes nothing; a block that fails (checksum, short read, bad type,
+// bad handle) is skipped and its error kept; status() is the first input's
+// (in input order) first error, an index-block error first
+// (TwoLevelIterator::status).
+class CompactionInput {
+ public:
+  struct Options {
+    const Comparator* comparator = nullptr;  // nullptr: InternalBytewiseComparator()
+    bool verify_checksums = true;            // Options::paranoid_checks
+    size_t prefetch_blocks = 64;             // per input and CRC batch
+    CrcMode crc_mode = CrcMode::kBatchAuto;
+    int device = 0;
+  };
+  // The images must outlive the reader (an mmap'd file, or pinned memory for
+  // zero-copy batches).
+  CompactionInput(const char* const* images, const size_t* sizes, size_t n, const Options& o);
+  ~CompactionInput();
+  CompactionInput(const CompactionInput&) = delete;
+  CompactionInput& operator=(const CompactionInput&) = delete;
+
+  void SeekToFirst();
+  bool Valid() const;
+  void Next();
+  std::string_view key() const;    // REQUIRES: Valid()
+  std::string_view value() const;  // REQUIRES: Valid()
+  Status status() const;
+  uint64_t CrcBatches() const;     // CRC batches issued (index blocks included)
+  uint64_t BlocksChecked() const;  // block CRCs computed
+
+ private:
+  struct Rep;
+  Rep* rep_;
+};
 
 }  // namespace table
 }  // namespace wipdb

@@ -82,6 +82,20 @@ int wsst_verify_tables(const char* const* images, const size_t* sizes, size_t n,
                        int bloom_bits, int crc_mode, int device, int* codes,
                        uint64_t* blocks_checked, uint64_t* bad_blocks);
 
+/* The compaction input path (kv/src/db/version_set.cc:1348-1373): the merged
+ * (InternalKeyComparator for WSST_KEYS_INTERNAL, else bytewise) entries of
+ * n table images, data blocks checked ahead of the merge prefetch_blocks per
+ * input per CRC batch (verify != 0: paranoid_checks).  Keys and values go
+ * to key_out / val_out (concatenated, lengths in key_lens / val_lens) in
+ * merge order, *nentries of them; *crc_batches (nullable) = CRC batches
+ * issued.  Returns the iterator's final status code; WSST_ERR_TOO_SMALL
+ * when a capacity is exceeded. */
+int wsst_merge_tables(const char* const* images, const size_t* sizes, size_t n, int key_format,
+                      int verify, size_t prefetch_blocks, int crc_mode, int device,
+                      char* key_out, size_t key_cap, uint32_t* key_lens, char* val_out,
+                      size_t val_cap, uint32_t* val_lens, size_t max_entries,
+                      uint64_t* nentries, uint64_t* crc_batches);
+
 /* kv::log::Writer::AddRecord for n records (concatenated + lengths) into a
  * fresh log (kv/src/db/log_writer.cc), every header CRC in one batch.
  * *out_size = image size; WSST_ERR_TOO_SMALL when it exceeds cap. */

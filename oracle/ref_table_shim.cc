@@ -16,7 +16,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <memory>
 #include <string>
+#include <vector>
 
 #include "db/dbformat.h"
 #include "kv/comparator.h"
@@ -26,6 +28,7 @@
 #include "kv/table.h"
 #include "kv/table_builder.h"
 #include "table/format.h"
+#include "table/merger.h"
 #include "util/file_reader_writer.h"
 
 namespace {
@@ -171,6 +174,62 @@ int ref_verify_table(const char* data, size_t n, int bloom_bits, size_t* blocks)
     delete t;
   }
   delete fp;
+  return rc;
+}
+
+// MakeInputIteratorKV (kv/src/db/version_set.cc:1348-1373) over n table
+// images: Table::Open with paranoid_checks = verify (TableCache::FindTable),
+// an error iterator for a table that fails to open, NewIterator with
+// verify_checksums = verify and fill_cache = false, NewMergingIterator under
+// InternalKeyComparator(Bytewise) (internal) or BytewiseComparator.  Writes
+// the merged entries like wsst_merge_tables; returns the status code
+// (-2 when a capacity is exceeded).
+int ref_merge_tables(const char* const* imgs, const size_t* sizes, size_t n, int internal,
+                     int verify, char* kout, size_t kcap, uint32_t* klens, char* vout,
+                     size_t vcap, uint32_t* vlens, size_t max_entries, size_t* nentries) {
+  kv::InternalKeyComparator icmp(kv::BytewiseComparator());
+  const kv::Comparator* cmp = internal ? static_cast<const kv::Comparator*>(&icmp)
+                                       : kv::BytewiseComparator();
+  kv::Options opt;
+  opt.comparator = cmp;
+  opt.paranoid_checks = verify != 0;
+  kv::ReadOptions ro;
+  ro.verify_checksums = verify != 0;
+  ro.fill_cache = false;
+  std::vector<std::unique_ptr<MemRandom>> files;
+  std::vector<kv::Table*> tables;
+  std::vector<kv::Iterator*> list;
+  for (size_t i = 0; i < n; ++i) {
+    files.emplace_back(new MemRandom(imgs[i], sizes[i]));
+    kv::Table* t = nullptr;
+    kv::Status s = kv::Table::Open(opt, files.back().get(), sizes[i], &t);
+    if (s.ok()) {
+      tables.push_back(t);
+      list.push_back(t->NewIterator(ro));
+    } else {
+      list.push_back(kv::NewErrorIterator(s));
+    }
+  }
+  kv::Iterator* it = kv::NewMergingIterator(cmp, list.data(), static_cast<int>(list.size()));
+  size_t k = 0, ko = 0, vo = 0;
+  int rc = 0;
+  for (it->SeekToFirst(); it->Valid(); it->Next(), ++k) {
+    const kv::Slice key = it->key(), val = it->value();
+    if (k >= max_entries || ko + key.size() > kcap || vo + val.size() > vcap) {
+      rc = -2;
+      break;
+    }
+    memcpy(kout + ko, key.data(), key.size());
+    memcpy(vout + vo, val.data(), val.size());
+    klens[k] = static_cast<uint32_t>(key.size());
+    vlens[k] = static_cast<uint32_t>(val.size());
+    ko += key.size();
+    vo += val.size();
+  }
+  *nentries = k;
+  if (rc == 0) rc = StatusCode(it->status());
+  delete it;
+  for (kv::Table* t : tables) delete t;
   return rc;
 }
 

@@ -7,6 +7,7 @@ device-generated) is compared with the compiled reference (oracle/_ref,
 8 threads) plus an oracle sample, and with the size-independent stitching
 property Extend(Extend(c, A), B) == Extend(c, A||B).
 """
+import ctypes
 import os
 import subprocess
 
@@ -159,10 +160,11 @@ def test_split_small_boundaries_and_mix(engine, oracle):
 
 
 def test_split_remainders(engine, oracle):
-    """HCRC_SPLIT_SMALL cuts a span whose rest after its first segment is
-    16..1024 bytes: the spans kernel leaves the partial CRC, the small
-    kernel finishes it.  Every start alignment, the cut's edges on both
-    sides, inits, masked output, mixed with small and long spans; and a
+    """HCRC_SPLIT_SMALL on spans just past one segment (a table block's
+    4 KiB + its last entry): the class-1 list runs them on the end-aligned
+    pipeline as a main segment + a batched front piece.  Every start
+    alignment, the piece's edges (1, 16, 17 chunks past 4 KiB), inits,
+    masked output, mixed with small and long spans; and a
     table-block-shaped host batch (4097..4225 B, SST-packed)."""
     rng = np.random.default_rng(41)
     buf = rng.integers(0, 256, 16 << 20, dtype=np.uint8)
@@ -514,3 +516,100 @@ def test_concurrent_host_batches_share_a_context(engine, oracle):
         np.testing.assert_array_equal(got[i], want[i])
     for i in range(4):
         np.testing.assert_array_equal(got[8 + i], want[i])
+
+
+def test_batch_multi_shards_on_one_device(oracle, golden_spans):
+    """hcrc_batch_multi_ex with a device listed several times: the threaded
+    byte-balanced split and the shared context (SURVEY 8e) on one MI355X;
+    every shard reports OK and the result equals the oracle."""
+    from wipdb_amd import batch_multi
+    g = golden_spans
+    rng = np.random.default_rng(8)
+    buf = rng.integers(0, 256, 6 << 20, dtype=np.uint8)
+    lens = rng.integers(0, 70000, 600).astype(np.uint32)
+    offs = np.array([int(rng.integers(0, buf.size - int(x))) for x in lens], np.uint64)
+    inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(buf, offs, lens, inits)
+    for devs in ([0, 0], [0, 0, 0, 0], [0] * 8):
+        got, rcs = batch_multi(devs, buf, offs, lens, inits, shard_status=True)
+        assert rcs == [0] * len(devs)
+        np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(batch_multi([0, 0], g["buf"], g["offsets"], g["lengths"],
+                                              g["inits"]), g["crc"])
+
+
+def test_batch_multi_failing_device_fails_its_shard_only(oracle):
+    """A shard on a device that does not exist returns HCRC_ERR_NO_DEVICE for
+    that shard alone; the other shard's results are still right."""
+    from wipdb_amd import _lib, batch_multi
+    rng = np.random.default_rng(9)
+    buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    lens = np.full(200, 4096, np.uint32)
+    offs = (np.arange(200, dtype=np.uint64) * 4096) % (buf.size - 4096)
+    want = oracle.batch(buf, offs, lens)
+    got, rcs = batch_multi([0, 4096], buf, offs, lens, shard_status=True)
+    assert rcs[0] == 0 and rcs[1] == _lib.HCRC_ERR_NO_DEVICE
+    n0 = 100  # equal lengths: the byte-balanced cut is the middle
+    np.testing.assert_array_equal(got[:n0], want[:n0])
+
+
+def test_calls_leave_the_current_device(engine):
+    """Every entry point restores the caller's current HIP device (a WipDB
+    flush thread or a torch process keeps its device)."""
+    import torch
+    before = torch.cuda.current_device()
+    rng = np.random.default_rng(10)
+    buf = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    offs = np.array([0, 100], np.uint64)
+    lens = np.array([5000, 300], np.uint32)
+    engine.batch(buf, offs, lens)
+    engine.batch_device(_t(buf), _t(offs), _t(lens))
+    torch.cuda.synchronize()
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    assert lib.hcrc_ctx_create(10_000, ctypes.byref(ctx)) == _lib.HCRC_ERR_NO_DEVICE
+    assert torch.cuda.current_device() == before
+
+
+def test_concurrent_host_batches_overlap(engine, oracle):
+    """flush, compaction and split threads call the engine at
+    once.  Synchronous host batches lease their own stream and staging slots,
+    so 8 threads run concurrently instead of queueing on one: their
+    aggregate throughput must exceed one thread's by a wide margin (and every
+    result is right)."""
+    import threading
+    import time
+    rng = np.random.default_rng(12)
+    nthr, calls = 8, 4
+    jobs = []
+    for t in range(nthr):
+        b = rng.integers(0, 256, size=24 << 20, dtype=np.uint8)
+        lens = rng.integers(4097, 4226, size=5000).astype(np.uint32)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 4)[:-1]]).astype(np.uint64)
+        jobs.append((b, offs, lens))
+    want = [oracle.batch(*j) for j in jobs[:2]]
+    for j in jobs:
+        engine.batch(*j)  # warm: every lane's staging allocated
+
+    def run(idx, out):
+        for _ in range(calls):
+            out[idx] = engine.batch(*jobs[idx])
+
+    one = [None]
+    t0 = time.perf_counter()
+    run(0, one)
+    t_one = (time.perf_counter() - t0) / calls
+    got = [None] * nthr
+    th = [threading.Thread(target=run, args=(i, got)) for i in range(nthr)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    t_all = time.perf_counter() - t0
+    np.testing.assert_array_equal(one[0], want[0])
+    np.testing.assert_array_equal(got[1], want[1])
+    speedup = (nthr * calls / t_all) / (1.0 / t_one)
+    print(f"aggregate speedup of {nthr} threads over one: {speedup:.2f}x")
+    assert speedup > 2.0, speedup

@@ -40,6 +40,9 @@ class RefTable:
                                            ctypes.c_int, ctypes.c_int, vp, sz]
         lib.ref_internal_compare.restype = ctypes.c_int
         lib.ref_internal_compare.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
+        lib.ref_merge_tables.restype = ctypes.c_int
+        lib.ref_merge_tables.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_int, vp, sz, vp, vp,
+                                         sz, vp, sz, ctypes.POINTER(sz)]
         lib.ref_filter_may_match.restype = ctypes.c_int
         lib.ref_filter_may_match.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz,
                                              ctypes.c_int, ctypes.c_int]
@@ -67,6 +70,26 @@ class RefTable:
         b = ctypes.create_string_buffer(img, len(img) or 1)
         nb = ctypes.c_size_t(0)
         return int(self.lib.ref_verify_table(b, len(img), bloom, ctypes.byref(nb)))
+
+    def merge(self, imgs, internal=True, verify=True):
+        """MakeInputIteratorKV over the images: (status code, entries)."""
+        bufs = [ctypes.create_string_buffer(i, len(i) or 1) for i in imgs]
+        ptrs = (ctypes.c_void_p * max(len(imgs), 1))(*[ctypes.addressof(b) for b in bufs])
+        sizes = np.array([len(i) for i in imgs] or [0], np.uint64)
+        cap = sum(len(i) for i in imgs) * 4 + 4096
+        ko, vo = ctypes.create_string_buffer(cap), ctypes.create_string_buffer(cap)
+        kl, vl = np.zeros(cap // 4, np.uint32), np.zeros(cap // 4, np.uint32)
+        ne = ctypes.c_size_t(0)
+        rc = self.lib.ref_merge_tables(ptrs, sizes.ctypes.data, len(imgs), int(internal),
+                                       int(verify), ko, cap, kl.ctypes.data, vo, cap,
+                                       vl.ctypes.data, cap // 4, ctypes.byref(ne))
+        assert rc >= 0
+        k, v, out, a, b = ko.raw, vo.raw, [], 0, 0
+        for i in range(ne.value):
+            out.append((k[a:a + int(kl[i])], v[b:b + int(vl[i])]))
+            a += int(kl[i])
+            b += int(vl[i])
+        return rc, out
 
     def read_block(self, img: bytes, off: int, size: int) -> int:
         b = ctypes.create_string_buffer(img, len(img) or 1)
@@ -297,6 +320,96 @@ def test_kv_builder_integration(mode):
     _run_kv_builder(mode)
 
 
+# ---- the compaction input path (MakeInputIteratorKV) -----------------------
+
+def _compaction_inputs(ntables: int, seed: int):
+    """Overlapping input tables of one compaction: every table draws user
+    keys from the whole range, some user keys appear in several tables with
+    different sequence numbers (newer in lower-numbered tables), 1 KiB
+    blocks so each table has many."""
+    rng = np.random.default_rng(seed)
+    users = sorted({b"user%010d" % int(x) for x in rng.integers(0, 10**9, 6000)})
+    per = [[] for _ in range(ntables)]
+    seq = 1 << 30
+    for u in users:
+        for t in sorted(rng.choice(ntables, size=int(rng.integers(1, 3)), replace=False)):
+            seq -= int(rng.integers(1, 50))
+            typ = 0 if rng.random() < 0.1 else 1
+            val = b"" if typ == 0 else bytes(rng.integers(32, 127, size=int(rng.integers(8, 200)),
+                                                          dtype=np.uint8))
+            per[int(t)].append((u + _tag(seq, typ), val))
+    ic = InternalOrder()
+    for p in per:
+        p.sort(key=ic)
+    return per
+
+
+class InternalOrder:
+    """sort key of InternalKeyComparator(BytewiseComparator)"""
+    def __call__(self, kv):
+        k = kv[0]
+        return (k[:-8], -int.from_bytes(k[-8:], "little"))
+
+
+def _merge_inputs(ref_table, ntables, seed, block_size=1024):
+    tables = _compaction_inputs(ntables, seed)
+    return tables, [ref_table.build(t, block_size, 16, 10, internal=True) for t in tables]
+
+
+@pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
+@pytest.mark.parametrize("prefetch", [1, 7, 64])
+def test_compaction_input_clean_matches_reference(ref_table, mode, prefetch):
+    """Merged entries of 6 overlapping inputs equal the reference's merging
+    iterator; the look-ahead checks batch many blocks per CRC call."""
+    tables, imgs = _merge_inputs(ref_table, 6, 70)
+    want_rc, want = ref_table.merge(imgs)
+    rc, got, batches = sst.merge_tables(imgs, prefetch_blocks=prefetch, crc_mode=mode)
+    assert rc == want_rc == sst.OK
+    assert got == want and len(got) == sum(len(t) for t in tables)
+    nblocks = sum(len(_handles(i)) - 2 for i in imgs)  # data blocks
+    assert batches <= 1 + -(-nblocks // (prefetch * 6)) * 6 + 6
+
+
+@pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
+def test_compaction_input_corruptions_match_reference(ref_table, mode):
+    """Seeded damage in data blocks, index blocks, footers and whole-image
+    truncation: the same entries (failed blocks skipped) and the same
+    status as the reference's merging iterator with paranoid_checks."""
+    tables, imgs = _merge_inputs(ref_table, 4, 71)
+    rng = np.random.default_rng(72)
+    seen = set()
+    for case in range(40):
+        cur = list(imgs)
+        for _ in range(int(rng.integers(1, 4))):
+            t = int(rng.integers(0, len(cur)))
+            b = bytearray(cur[t])
+            kind = case % 4
+            if kind == 0 or kind == 1:  # anywhere in the body (mostly data blocks)
+                b[int(rng.integers(0, len(b) - 48))] ^= 1 << int(rng.integers(0, 8))
+            elif kind == 2:  # the index block
+                io, isz = _handles(cur[t])[1]
+                b[io + int(rng.integers(0, isz + 5))] ^= 0x04
+            else:  # truncation or a footer byte
+                if rng.random() < 0.5:
+                    b = b[:int(rng.integers(0, len(b)))]
+                else:
+                    b[len(b) - 1 - int(rng.integers(0, 48))] ^= 0x80
+            cur[t] = bytes(b)
+        want_rc, want = ref_table.merge(cur)
+        rc, got, _ = sst.merge_tables(cur, prefetch_blocks=int(rng.integers(1, 40)), crc_mode=mode)
+        assert (rc, got) == (want_rc, want), case
+        seen.add(want_rc)
+    assert {sst.CRC_MISMATCH, sst.CORRUPTION} <= seen
+
+
+def test_compaction_input_without_checksums_matches_reference(ref_table):
+    """paranoid_checks off: no block CRC at all, the same merged stream."""
+    _, imgs = _merge_inputs(ref_table, 5, 73)
+    want_rc, want = ref_table.merge(imgs, verify=False)
+    rc, got, batches = sst.merge_tables(imgs, verify=False, crc_mode=sst.CRC_BATCH_CPU)
+    assert (rc, got) == (want_rc, want) and batches == 0
+
+
 # ---- read side --------------------------------------------------------------
 
 def _handles(img: bytes):
@@ -484,3 +597,38 @@ def test_gpu_internal_key_compaction_outputs(ref_table, engine):
 def test_gpu_kv_builder_integration(engine):
     """The reference-side integration with every block CRC on the MI355X."""
     _run_kv_builder(sst.CRC_BATCH_GPU)
+
+
+@pytest.mark.gpu
+def test_gpu_verify_pinned_images_zero_copy(ref_table, engine):
+    """Table images in pinned memory (sst.PinnedImages): the verify batch
+    reads them zero-copy; statuses equal the reference's for clean and
+    corrupted images."""
+    tables = [kv_8binsert(1500, 300 + i) for i in range(8)]
+    imgs = [ref_table.build(t, bloom=10) for t in tables]
+    bad = bytearray(imgs[3])
+    bad[2000] ^= 8
+    imgs[3] = bytes(bad)
+    want = [ref_table.verify(i, 10) for i in imgs]
+    with sst.PinnedImages(imgs) as pin:
+        rc, codes = sst.verify_tables_at(pin.addrs, pin.sizes, 10, sst.CRC_BATCH_GPU)
+    assert codes == want and want[3] == sst.CRC_MISMATCH
+
+
+@pytest.mark.gpu
+def test_gpu_compaction_input_matches_reference(ref_table, engine):
+    """The compaction input path with every look-ahead CRC batch on the
+    MI355X: clean and damaged inputs give the reference's entries and status."""
+    _, imgs = _merge_inputs(ref_table, 8, 74)
+    want = ref_table.merge(imgs)
+    rc, got, batches = sst.merge_tables(imgs, prefetch_blocks=64, crc_mode=sst.CRC_BATCH_GPU)
+    assert (rc, got) == want and batches > 1
+    rng = np.random.default_rng(75)
+    for case in range(6):
+        cur = list(imgs)
+        t = int(rng.integers(0, len(cur)))
+        b = bytearray(cur[t])
+        b[int(rng.integers(0, len(b) - 48))] ^= 0x10
+        cur[t] = bytes(b)
+        rc, got, _ = sst.merge_tables(cur, prefetch_blocks=16, crc_mode=sst.CRC_BATCH_GPU)
+        assert (rc, got) == ref_table.merge(cur), case

@@ -74,29 +74,19 @@ constexpr uint32_t kFlagMask = 0x2;
 // Size classes (HCRC_SPLIT_SMALL).  A span of n bytes at address a covers
 // f = (a % 16 + n) / 16 full chunks of its 16-byte grid.  Class 4 (16-lane
 // groups, 4 spans per wave iteration): f <= 64; class 2 (32-lane groups):
-// f <= 128; class 1: the rest, segment by segment.  A class-1 span whose
-// chunks beyond its first 256 number 1..128 (a table block: 4 KiB + its last
-// entry + the type byte) is cut: the class-1 kernel writes the partial CRC
-// of its first 256 chunks and the remainder -- 16-aligned, so no head --
-// goes to class 2 or 4 as a continuation.
+// f <= 128; class 1: the rest, on the end-aligned pipeline of the spans
+// kernel (table blocks as a main segment + a batched front piece).
 constexpr uint32_t kClass4Chunks = 64;
 constexpr uint32_t kClass2Chunks = 128;
-constexpr uint32_t kListCut = 0x80000000u;   // id word: class-1 entry stops after its first segment
-constexpr uint32_t kListIdMask = 0x7fffffffu;
-constexpr uint32_t kLinkClass4 = 0x80000000u;  // link word: the remainder is in the class-4 list
-constexpr uint64_t kMaxListSpans = uint64_t(1) << 30;  // link positions are 30 bits
+constexpr uint64_t kMaxListSpans = uint64_t(1) << 31;  // list ids are 32 bits
 
 // One size-class list (struct of arrays, device memory); `count` is a device
-// counter the partition kernel fills.  A cut class-1 entry's `link` names its
-// remainder's entry (kLinkClass4 | position); the class-1 kernel writes the
-// partial CRC into that entry's init column, which the class-2/4 kernel
-// (launched after it) then continues from.
+// counter the partition kernel fills.
 struct SpanList {
-  uint64_t* off;   // byte offset of the (remainder's) first byte from the batch base
+  uint64_t* off;   // byte offset of the span's first byte from the batch base
   uint32_t* len;   // bytes (verify: including the type byte)
-  uint32_t* init;  // init_crc (remainders: the partial CRC, written by the class-1 kernel)
-  uint32_t* id;    // output slot | kListCut
-  uint32_t* link;  // class 1, cut: the remainder's list entry
+  uint32_t* init;  // init_crc
+  uint32_t* id;    // output slot
   uint32_t* count;
 };
 

@@ -40,7 +40,7 @@
 // tail chunk and stored trailer come in with its segment as one-lane DMAs
 // into per-wave aux pieces.  Every vector-memory instruction is a DMA or a
 // result store, counted by hand (s_waitcnt vmcnt) -- see the issue order in
-// run1().
+// run_ea().
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -384,33 +384,16 @@ struct ListSrc {
   const uint32_t* len;
   const uint32_t* init;
   const uint32_t* id;
-  const uint32_t* link;
   uint64_t count;
   __device__ __forceinline__ SpanD get(uint64_t s) const {
-    const uint32_t w = id[s];
-    const uint32_t lk = (w & kListCut) ? (link[s] & (kLinkClass4 | 0x3fffffffu)) | kLinkValid : 0u;
-    return SpanD{off[s], len[s], init[s], lk, w & kListIdMask};
+    return SpanD{off[s], len[s], init[s], 0u, id[s]};
   }
 };
 
 // ---------------------------------------------------------------------------
-// Segments of a span (uniform).
+// Chunk geometry of the size-class lists' spans (run_g): a grid that starts
+// at the span's first 16-byte-aligned chunk, with a ragged tail.
 // ---------------------------------------------------------------------------
-// (the size-class list kernels' segments: a chunk grid that starts at the
-// span's first 16-byte-aligned chunk, with a ragged tail)
-constexpr uint32_t kSegValid = 1u, kSegFirst = 2u, kSegLast = 4u, kSegCut = 8u;
-
-struct Seg {
-  uint64_t a0;    // offset of the segment's first chunk (16-byte aligned address)
-  uint32_t nc;    // full chunks (0..256)
-  uint32_t h;     // first segment: bytes of the first chunk in front of the span
-  uint32_t o, e;  // last segment: tail bytes [o, e) of the chunk at a0 + 16 nc
-  uint32_t flags;
-  uint32_t init;  // first segment: the span's init
-  uint32_t link;  // cut: where its partial CRC goes
-  uint64_t id;    // output slot
-};
-
 // The chunk geometry of a span at absolute address abs: h bytes of its first
 // chunk lie in front of it, f full chunks, t tail bytes (for f == 0, the
 // span's end inside chunk 0; 0 for an empty span).
@@ -424,54 +407,11 @@ struct Geo {
   }
 };
 
-// A span being walked segment by segment (G = 1).
-struct Walk {
-  uint64_t a0, id;
-  uint32_t f, h, t, init, k, nseg, link;
-  bool cut, valid;
-
-  __device__ __forceinline__ void start(const uint8_t* base, const SpanD& d) {
-    const Geo g(reinterpret_cast<uint64_t>(base) + d.a, d.n);
-    h = g.h;
-    f = g.f;
-    t = g.t;
-    a0 = d.a - h;
-    init = d.init;
-    id = d.id;
-    link = d.link;
-    k = 0;
-    cut = (d.link & kLinkValid) != 0u;
-    nseg = cut ? 1u : (f == 0u ? 1u : (f + kSegChunks - 1u) / kSegChunks);
-    valid = true;
-  }
-  __device__ __forceinline__ Seg next() {
-    Seg g;
-    const bool last = k + 1u == nseg;
-    g.a0 = a0 + static_cast<uint64_t>(k) * (kSegChunks * 16u);
-    const uint32_t left = f - k * kSegChunks;
-    g.nc = left < kSegChunks ? left : kSegChunks;
-    g.h = k == 0u ? h : 0u;
-    // the tail: bytes [0, t) of the chunk after the last full one; a span
-    // inside one chunk (f == 0) is all tail, bytes [h, t)
-    g.o = f == 0u ? h : 0u;
-    g.e = (last && !cut) ? t : 0u;
-    g.flags = kSegValid | (k == 0u ? kSegFirst : 0u) | (last ? kSegLast : 0u) | (cut ? kSegCut : 0u);
-    g.init = init;
-    g.link = link;
-    g.id = id;
-    if (last) valid = false;
-    ++k;
-    return g;
-  }
-};
-
 // The register that must enter a span's first chunk (h bytes in front of
 // the span): ~init * x^(-8h).  Uniform.
 __device__ __forceinline__ uint32_t head_register(uint32_t l, uint32_t init, uint32_t h) {
   return uni(init == 0u ? lds_ld(MiscAddr(kMiscHead0 + h)) : unshift(l, ~init, h));
 }
-
-// Byte mask of word ww of a chunk whose first h bytes are not the span's.
 
 // LE32 at byte e (< 16) of the 32 bytes lo || hi (a verify trailer).
 __device__ __forceinline__ uint32_t le32_at(const u32x4& lo, const u32x4& hi, uint32_t e) {
@@ -579,134 +519,6 @@ struct Pipe {
 };
 
 // ---------------------------------------------------------------------------
-// G = 1: one segment per wave iteration, spans of any length.  Issue order
-// of vector-memory instructions per wave:
-//   DMA(seg i) ... result store(seg i-1) ... DMA(seg i+1) ...
-// so waiting for seg i's DMA is vmcnt(1) when a store followed it, else 0.
-// OUT: 0 = CRC (masked with kFlagMask), 1 = verify status byte.  A cut span
-// (class-1 list entry) writes its unmasked partial CRC into the init column
-// of its remainder's class-2 / class-4 list entry (rem2 / rem4).
-// ---------------------------------------------------------------------------
-template <int OUT, typename Src>
-__device__ __forceinline__ void run1(const Src& src, void* out, uint32_t flags, uint32_t* rem2,
-                                     uint32_t* rem4, const uint8_t* image) {
-  const uint32_t l = threadIdx.x & 63u;
-  const uint32_t w = uni(threadIdx.x >> 6);
-  const uint64_t count = src.count;
-  if (static_cast<uint64_t>(blockIdx.x) * 16u >= count) return;  // no block of work
-  load_image(image, w, l);
-  const Lane lk = make_lane<1>(l);
-  Pipe pp;
-  pp.init(l, w);
-  const bool msk = (flags & kFlagMask) != 0u;
-  const uint64_t sbase = reinterpret_cast<uint64_t>(src.base);
-
-  // the prefetched next span: its descriptor loads are issued an iteration
-  // before it is used, so their latency hides behind a segment
-  struct Pref {
-    SpanD d;
-    bool valid;
-  };
-  auto prefetch = [&](Pref& p) {
-    const uint64_t s = grab_units<1>(l);
-    p.valid = s < count;
-    if (p.valid) p.d = src.get(s);
-  };
-  auto issue = [&](const Seg& g) {
-    if (g.nc != 0u) pp.issue<4>(sbase + g.a0, 0u, kSegChunks, g.nc);
-    if (g.flags & kSegLast)
-      pp.issue_end(sbase + g.a0 + 16u * g.nc, 0u, g.e > g.o, OUT == 1 && !(g.flags & kSegCut), g.e);
-  };
-
-  Walk wk;
-  Pref pf;
-  prefetch(pf);
-  if (!pf.valid) return;
-  wk.start(src.base, pf.d);
-  prefetch(pf);
-  Seg cur = wk.next();
-  issue(cur);
-  uint32_t chain = 0;  // register carried between the segments of a span
-  bool stored_prev = false;
-
-  for (;;) {
-    if (stored_prev) wait_vm<1>();
-    else wait_vm<0>();
-    uint32_t W[16];
-    pp.read(W);
-    u32x4 tail{0, 0, 0, 0}, next{0, 0, 0, 0};
-    if (cur.flags & kSegLast) {
-      tail = pp.piece(kAuxTail);
-      if (OUT == 1 && cur.e > 12u) next = pp.piece(kAuxNext);
-    }
-    pp.release();
-    // the next segment: the rest of this span, or the prefetched span
-    Seg nxt;
-    nxt.flags = 0;
-    bool took_pf = false;
-    if (wk.valid) {
-      nxt = wk.next();
-    } else if (pf.valid) {
-      wk.start(src.base, pf.d);
-      took_pf = true;
-      nxt = wk.next();
-    }
-    if (nxt.flags & kSegValid) issue(nxt);
-
-    // ---- CRC of the current segment ----
-    uint32_t R;
-    if (cur.nc == 0u) {
-      R = ~cur.init;  // a span inside one chunk: all of it is tail
-    } else {
-      const uint32_t inj = (cur.flags & kSegFirst) ? head_register(l, cur.init, cur.h) : chain;
-      if (cur.nc == kSegChunks && cur.h == 0u) {
-        W[0] ^= l == 0u ? inj : 0u;
-      } else {
-        // chunk i of lane l is segment chunk 4l + i - (256 - nc): zero the
-        // ones in front of the segment, mask the first h bytes of chunk 0
-        // and put the register there
-        const int32_t base = static_cast<int32_t>(kSegChunks - cur.nc);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int32_t ci = static_cast<int32_t>(4u * l) + i - base;
-#pragma unroll
-          for (uint32_t ww = 0; ww < 4; ++ww)
-            W[4 * i + ww] &= ci < 0 ? 0u : (ci == 0 ? head_mask(cur.h, ww) : ~0u);
-          W[4 * i] ^= ci == 0 ? inj : 0u;
-        }
-      }
-      R = fold<1>(lk, l, scan(lk, W))[0];
-    }
-
-    bool did_store = false;
-    if (cur.flags & kSegLast) {
-      tail = u32x4{uni(tail.x), uni(tail.y), uni(tail.z), uni(tail.w)};
-      if (cur.e > cur.o) R = feed_tail(lk, l, R, tail, cur.o, cur.e);
-      const uint32_t crc = ~R;
-      did_store = true;
-      if (l == 0u) {
-        if (cur.flags & kSegCut) {
-          // the partial CRC continues in the remainder's list entry
-          uint32_t* dst = (cur.link & kLinkClass4) ? rem4 : rem2;
-          dst[cur.link & 0x3fffffffu] = crc;
-        } else if (OUT == 1) {
-          const uint32_t stored = le32_at(tail, next, cur.e);
-          static_cast<uint8_t*>(out)[cur.id] = unmask_crc(stored) == crc ? 1u : 0u;
-        } else {
-          static_cast<uint32_t*>(out)[cur.id] = msk ? mask_crc(crc) : crc;
-        }
-      }
-    } else {
-      chain = R;
-    }
-    stored_prev = did_store;
-
-    if (!(nxt.flags & kSegValid)) break;
-    if (took_pf) prefetch(pf);
-    cur = nxt;
-  }
-}
-
 // The descriptor / strided / verify pipeline: the END-ALIGNED GRID
 // (crc32c_walk.h: the grid, segments, pieces and their DMA sources).
 // Main path: zero the window chunks in front of the segment (front, uniform)
@@ -1225,25 +1037,24 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
 }
 
 // A size-class list (HCRC_SPLIT_SMALL): G = 1 takes the spans of more than
-// 128 chunks (cut ones write their partial CRC into rem2 / rem4, the init
-// columns of the class-2 / class-4 lists), G = 2 / 4 the spans and
-// remainders of at most 128 / 64 chunks.  OUT: 0 = CRCs into out (u32),
-// 1 = verify statuses into out (u8).
+// 128 chunks on the end-aligned pipeline (table blocks as main segment +
+// front piece), G = 2 / 4 the spans of at most 128 / 64 chunks, several per
+// wave iteration.  OUT: 0 = CRCs into out (u32, masked with kFlagMask),
+// 1 = verify statuses into out (u8; the list lengths include the type byte).
 template <int G, int OUT>
 __global__ __launch_bounds__(kThreads) void crc32c_lds_list_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ init,
-    const uint32_t* __restrict__ id, const uint32_t* __restrict__ link,
-    const uint32_t* __restrict__ count, void* out, uint32_t* rem2, uint32_t* rem4, uint32_t flags,
-    const uint8_t* __restrict__ image) {
-  const ListSrc src{base, off, len, init, id, link, *count};
-  if constexpr (G == 1) run1<OUT>(src, out, flags, rem2, rem4, image);
+    const uint32_t* __restrict__ id, const uint32_t* __restrict__ count, void* out,
+    uint32_t flags, const uint8_t* __restrict__ image) {
+  const ListSrc src{base, off, len, init, id, *count};
+  if constexpr (G == 1) run_ea<OUT>(src, out, flags, image);
   else run_g<G, OUT>(src, out, flags, image);
 }
-#define WIPDB_LIST_KERNEL(G, OUT)                                                              \
-  template __global__ void crc32c_lds_list_kernel<G, OUT>(                                     \
-      const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, const uint32_t*,     \
-      const uint32_t*, const uint32_t*, void*, uint32_t*, uint32_t*, uint32_t, const uint8_t*)
+#define WIPDB_LIST_KERNEL(G, OUT)                                                          \
+  template __global__ void crc32c_lds_list_kernel<G, OUT>(                                 \
+      const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, const uint32_t*, \
+      const uint32_t*, void*, uint32_t, const uint8_t*)
 WIPDB_LIST_KERNEL(1, 0);
 WIPDB_LIST_KERNEL(2, 0);
 WIPDB_LIST_KERNEL(4, 0);
@@ -1257,38 +1068,18 @@ WIPDB_LIST_KERNEL(4, 1);
 // contiguous range of the batch twice: counts per class, one global atomic
 // per class to reserve its slices, then writes the entries (wave-ordered
 // through a ballot prefix), so each list keeps the batch's memory order
-// piecewise.  A cut span's class-1 entry links to its remainder's entry.
+// piecewise.
 // ---------------------------------------------------------------------------
 constexpr int kPartThreads = 256;
 
-struct Classified {
-  uint32_t cls;   // 1, 2 or 4
-  bool cut;       // class 1: a remainder entry too
-  uint32_t rcls;  // the remainder's class
-  uint64_t roff;  // remainder: offset of its first byte
-  uint32_t rlen;
-};
-
-__device__ __forceinline__ Classified classify(const uint8_t* base, uint64_t off, uint32_t n) {
-  Classified c;
+// The class of a span of n bytes at address base + off: f = (a % 16 + n) / 16
+// full chunks of its 16-byte grid; class 4: f <= 64, class 2: f <= 128,
+// class 1: the rest.
+__device__ __forceinline__ int class_slot(const uint8_t* base, uint64_t off, uint32_t n) {
   const uint32_t h = static_cast<uint32_t>((reinterpret_cast<uint64_t>(base) + off) & 15u);
-  const uint32_t hn = h + n;
-  const uint32_t f = hn >> 4;
-  c.cls = f <= kClass4Chunks ? 4u : (f <= kClass2Chunks ? 2u : 1u);
-  c.cut = f > kSegChunks && f - kSegChunks <= kClass2Chunks;
-  c.rcls = 0;
-  c.roff = 0;
-  c.rlen = 0;
-  if (c.cut) {
-    const uint32_t first = kSegChunks * 16u - h;  // bytes of the first segment
-    c.roff = off + first;
-    c.rlen = n - first;
-    c.rcls = (hn - kSegChunks * 16u) >> 4 <= kClass4Chunks ? 4u : 2u;
-  }
-  return c;
+  const uint32_t f = (h + n) >> 4;
+  return f <= kClass4Chunks ? 2 : (f <= kClass2Chunks ? 1 : 0);
 }
-
-__device__ __forceinline__ int class_slot(uint32_t cls) { return cls == 1u ? 0 : (cls == 2u ? 1 : 2); }
 
 __global__ __launch_bounds__(kPartThreads) void crc32c_lds_partition_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
@@ -1303,11 +1094,8 @@ __global__ __launch_bounds__(kPartThreads) void crc32c_lds_partition_kernel(
   __syncthreads();
   // pass 1: count
   uint32_t mine[3] = {0, 0, 0};
-  for (uint64_t s = lo + tid; s < hi; s += kPartThreads) {
-    const Classified c = classify(base, offsets[s], lengths[s] + extra);
-    ++mine[class_slot(c.cls)];
-    if (c.cut) ++mine[class_slot(c.rcls)];
-  }
+  for (uint64_t s = lo + tid; s < hi; s += kPartThreads)
+    ++mine[class_slot(base, offsets[s], lengths[s] + extra)];
 #pragma unroll
   for (int k = 0; k < 3; ++k)
     if (mine[k]) atomicAdd(&cnt[k], mine[k]);
@@ -1324,46 +1112,31 @@ __global__ __launch_bounds__(kPartThreads) void crc32c_lds_partition_kernel(
   for (uint64_t s0 = wbase; s0 < hi; s0 += kPartThreads) {
     const uint64_t s = s0 + lane;
     const bool live = s < hi;
-    Classified c{};
     uint64_t off = 0;
     uint32_t n = 0, ini = 0;
+    int cls = -1;
     if (live) {
       off = offsets[s];
       n = lengths[s] + extra;
       ini = inits ? inits[s] : 0u;
-      c = classify(base, off, n);
+      cls = class_slot(base, off, n);
     }
-    uint32_t pa = 0, pb = 0;  // this lane's entry positions (primary, remainder)
+    uint32_t pa = 0;  // this lane's entry position
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const uint32_t cls = k == 0 ? 1u : (k == 1 ? 2u : 4u);
-      const bool a = live && c.cls == cls;
-      const bool b = live && c.cut && c.rcls == cls;
-      const uint64_t ma = __builtin_amdgcn_ballot_w64(a);
-      const uint64_t mb = __builtin_amdgcn_ballot_w64(b);
-      const uint32_t na = __builtin_popcountll(ma), nb = __builtin_popcountll(mb);
-      if (na + nb == 0u) continue;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(cls == k);
+      if (m == 0u) continue;
       uint32_t p0 = 0;
-      if (lane == 0u) p0 = atomicAdd(&pos[k], na + nb);
+      if (lane == 0u) p0 = atomicAdd(&pos[k], static_cast<uint32_t>(__builtin_popcountll(m)));
       p0 = __builtin_amdgcn_readfirstlane(p0);
-      if (a) pa = p0 + __builtin_popcountll(ma & below);
-      if (b) pb = p0 + na + __builtin_popcountll(mb & below);
+      if (cls == k) pa = p0 + __builtin_popcountll(m & below);
     }
     if (live) {
-      const SpanList& L = c.cls == 1u ? l1 : (c.cls == 2u ? l2 : l4);
+      const SpanList& L = cls == 0 ? l1 : (cls == 1 ? l2 : l4);
       L.off[pa] = off;
       L.len[pa] = n;
       L.init[pa] = ini;
-      L.id[pa] = static_cast<uint32_t>(s) | (c.cut ? kListCut : 0u);
-      L.link[pa] = c.cut ? (pb | (c.rcls == 4u ? kLinkClass4 : 0u)) : 0u;
-      if (c.cut) {
-        const SpanList& R = c.rcls == 2u ? l2 : l4;
-        R.off[pb] = c.roff;
-        R.len[pb] = c.rlen;
-        R.init[pb] = 0u;  // the class-1 kernel writes the partial CRC here
-        R.id[pb] = static_cast<uint32_t>(s);
-        R.link[pb] = 0u;
-      }
+      L.id[pa] = static_cast<uint32_t>(s);
     }
   }
 }

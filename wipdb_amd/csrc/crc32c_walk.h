@@ -18,10 +18,9 @@ struct SpanD {
   uint64_t a;      // offset of the first byte from the source base
   uint32_t n;      // bytes
   uint32_t init;   // Extend's init_crc
-  uint32_t link;   // class-1 list entry cut after its first segment: kLinkValid | remainder
+  uint32_t link;   // (unused: keeps the layout of the list sources)
   uint64_t id;     // output slot
 };
-constexpr uint32_t kLinkValid = 0x40000000u;  // SpanD.link: the span is cut (link in low bits)
 
 // Byte mask of word ww of chunk 0: its first h bytes are not the span's.
 WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {

@@ -40,9 +40,8 @@ __global__ void crc32c_lds_verify_kernel(const uint8_t*, const uint64_t*, const 
                                          uint8_t*, uint64_t, const uint8_t*);
 template <int G, int OUT>
 __global__ void crc32c_lds_list_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
-                                       const uint32_t*, const uint32_t*, const uint32_t*,
-                                       const uint32_t*, void*, uint32_t*, uint32_t*, uint32_t,
-                                       const uint8_t*);
+                                       const uint32_t*, const uint32_t*, const uint32_t*, void*,
+                                       uint32_t, const uint8_t*);
 __global__ void crc32c_lds_partition_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                             const uint32_t*, uint64_t, uint32_t, SpanList,
                                             SpanList, SpanList);
@@ -203,18 +202,36 @@ std::map<uintptr_t, HostRange>& HostRanges() {
   return *m;
 }
 
-// Device address of [lo, hi) when the whole range lies inside ONE range
-// pinned or registered through this library; nullptr otherwise (pageable
-// memory, or spans spread over several allocations -- those are staged).
-const uint8_t* MappedRange(const uint8_t* lo, const uint8_t* hi) {
+// The device-side base for a host batch whose every span lies inside a range
+// pinned or registered through this library (zero-copy), or nullptr (some
+// span is in pageable memory, or straddles two ranges: the batch is staged).
+// Each span is looked up -- the ranges are sorted by start and a batch's
+// spans usually walk them in order, so the last hit is tried first.  Spans in
+// one range translate through its device address; spans over several
+// ranges need every range identity-mapped (device address == host address,
+// what ROCm gives pinned and registered memory under unified addressing).
+const uint8_t* MappedSpans(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+                           size_t n) {
   std::lock_guard<std::mutex> lk(g_host_mu);
   auto& m = HostRanges();
-  auto it = m.upper_bound(reinterpret_cast<uintptr_t>(lo));
-  if (it == m.begin()) return nullptr;
-  --it;
-  const uintptr_t start = it->first;
-  if (reinterpret_cast<uintptr_t>(hi) > start + it->second.bytes) return nullptr;
-  return it->second.dev + (reinterpret_cast<uintptr_t>(lo) - start);
+  if (m.empty() || n == 0) return nullptr;
+  auto hit = m.end();
+  bool several = false, identity = true;
+  for (size_t i = 0; i < n; ++i) {
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(base + offsets[i]);
+    const uintptr_t hi = lo + lengths[i];
+    if (hit == m.end() || lo < hit->first || hi > hit->first + hit->second.bytes) {
+      auto it = m.upper_bound(lo);
+      if (it == m.begin()) return nullptr;
+      --it;
+      if (hi > it->first + it->second.bytes) return nullptr;
+      if (hit != m.end() && it != hit) several = true;
+      hit = it;
+      identity = identity && reinterpret_cast<uintptr_t>(hit->second.dev) == hit->first;
+    }
+  }
+  if (several) return identity ? base : nullptr;
+  return hit->second.dev - (hit->first - reinterpret_cast<uintptr_t>(base));
 }
 
 }  // namespace
@@ -299,17 +316,16 @@ int LdsGrid(hcrc_ctx* ctx, size_t count) {
 int Launched() { return hipGetLastError() == hipSuccess ? HCRC_OK : HCRC_ERR_LAUNCH; }
 
 // Size classes of a batch (HCRC_SPLIT_SMALL, crc32c_lds.h): a partition pass
-// writes three lists, then the class-1 kernel (which writes the partial CRCs
-// of the spans it cuts) and the class-2 and class-4 kernels (which continue
-// them) run in stream order.  Stream-ordered scratch, so concurrent calls on
-// different streams never share it.  out_kind 0: CRCs (masked when `mask`)
+// writes three lists, then the class-1, class-2 and class-4 kernels run in
+// stream order.  Stream-ordered scratch, so concurrent calls on different
+// streams never share it.  out_kind 0: CRCs (masked when `mask`)
 // into u32 out; 1: verify statuses into u8 out.
 int LaunchClasses(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
                   const uint32_t* init, void* out, size_t n, int out_kind, bool mask,
                   hipStream_t st) {
   // scratch: 3 lists of n entries -- the u64 offset columns first (8-byte
-  // aligned), then the u32 columns (len, init, id, link), the 3 counters
-  const size_t bytes = n * (3 * 8 + 3 * 16) + 16;
+  // aligned), then the u32 columns (len, init, id), the 3 counters
+  const size_t bytes = n * (3 * 8 + 3 * 12) + 16;
   uint8_t* scratch = nullptr;
   HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), bytes, ctx->scratch_pool,
                                     st));
@@ -323,8 +339,7 @@ int LaunchClasses(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const
     l.len = reinterpret_cast<uint32_t*>(p);
     l.init = l.len + n;
     l.id = l.init + n;
-    l.link = l.id + n;
-    p += n * 16;
+    p += n * 12;
   }
   uint32_t* counts = reinterpret_cast<uint32_t*>(p);
   for (int k = 0; k < 3; ++k) L[k].count = counts + k;
@@ -339,13 +354,12 @@ int LaunchClasses(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const
   }
   const uint32_t kf = mask ? lk::kFlagMask : 0u;
   const dim3 grid(ctx->num_cu), blk(lk::kThreads);
-  // class 1 first: its cut entries write the class-2/4 remainders' inits
   auto launch = [&](auto kernel, const lk::SpanList& l) {
     hipLaunchKernelGGL(kernel, grid, blk, lk::kLdsBytes, st, base,
                        static_cast<const uint64_t*>(l.off), static_cast<const uint32_t*>(l.len),
                        static_cast<const uint32_t*>(l.init), static_cast<const uint32_t*>(l.id),
-                       static_cast<const uint32_t*>(l.link), static_cast<const uint32_t*>(l.count),
-                       out, L[1].init, L[2].init, kf, static_cast<const uint8_t*>(ctx->d_image));
+                       static_cast<const uint32_t*>(l.count), out, kf,
+                       static_cast<const uint8_t*>(ctx->d_image));
   };
   if (rc == HCRC_OK) {
     if (out_kind) {
@@ -388,16 +402,16 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
 }
 
 // Whether a host piece should go through the size classes: enough spans of
-// at most 2 KiB (WAL records, small meta blocks) or just over 4 KiB (table
-// blocks: 4 KiB plus their last entry) to pay for the partition pass and
-// the two extra launches.  Span i's address mod 16 is base + offsets[i]'s.
+// at most 2 KiB (WAL records, small meta blocks) to pay for the partition
+// pass and the two extra launches (table blocks -- 4 KiB plus their last
+// entry -- need no classes: the spans kernel batches their front pieces).
+// Span i's address mod 16 is base + offsets[i]'s.
 constexpr size_t kAutoSplitMin = 256;
 int AutoSplit(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, size_t n) {
   size_t hits = 0;
   for (size_t i = 0; i < n && hits < kAutoSplitMin; ++i) {
     const uint32_t h = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(base) + offsets[i]) & 15u);
-    const uint32_t f = (h + lengths[i]) >> 4;
-    hits += f <= lk::kClass2Chunks || (f > lk::kSegChunks && f - lk::kSegChunks <= lk::kClass2Chunks);
+    hits += ((h + lengths[i]) >> 4) <= lk::kClass2Chunks;
   }
   return hits >= kAutoSplitMin ? HCRC_SPLIT_SMALL : 0;
 }
@@ -480,16 +494,8 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
   LaneLease lane(ctx);
   int rc = lane.Staging();
   if (rc) return rc;
-  {
-    uint64_t lo = ~uint64_t(0), hi = 0;
-    for (size_t i = 0; i < count; ++i) {
-      lo = std::min(lo, offsets[i]);
-      hi = std::max(hi, offsets[i] + lengths[i]);
-    }
-    const uint8_t* dev = MappedRange(base + lo, base + hi);
-    if (dev)
-      return BatchZeroCopy(ctx, lane, dev - lo, base, offsets, lengths, inits, out, count, flags);
-  }
+  if (const uint8_t* dev = MappedSpans(base, offsets, lengths, count))
+    return BatchZeroCopy(ctx, lane, dev, base, offsets, lengths, inits, out, count, flags);
   const hipStream_t st = lane->stream;
   size_t i = 0;
   int k = 0;

@@ -3,8 +3,14 @@
 // batches, and the span-batch helper of span_crc.h.
 #include "../../include/wipdb/table.h"
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <algorithm>
+#include <map>
+#include <new>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "../../include/hip_crc32c_batch.h"
@@ -124,6 +130,110 @@ TableOptions InternalKeyTableOptions(TableOptions base) {
   return base;
 }
 
+namespace {
+
+// Pinned host buffers (hcrc_host_alloc) recycled process-wide: pinning is
+// slow (milliseconds per MiB), table builders are many and short-lived.
+class PinnedPool {
+ public:
+  static PinnedPool& Get() {
+    static PinnedPool* p = new PinnedPool;
+    return *p;
+  }
+  // A buffer of at least `bytes` (capacity in *cap), or nullptr when
+  // pinned memory is unavailable (no device).
+  char* Take(size_t bytes, size_t* cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = free_.lower_bound(bytes);
+      if (it != free_.end() && it->first <= 2 * bytes) {
+        char* p = it->second;
+        *cap = it->first;
+        held_ -= it->first;
+        free_.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hcrc_host_alloc(bytes, &p) != HCRC_OK) return nullptr;
+    *cap = bytes;
+    return static_cast<char*>(p);
+  }
+  void Give(char* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (held_ + cap <= kMaxHeld) {
+        free_.emplace(cap, p);
+        held_ += cap;
+        return;
+      }
+    }
+    (void)hcrc_host_free(p);
+  }
+
+ private:
+  static constexpr size_t kMaxHeld = size_t(1) << 30;
+  std::mutex mu_;
+  std::multimap<size_t, char*> free_;
+  size_t held_ = 0;
+};
+
+// The builder's write buffer: pinned in the MI355X modes (so the batch of its
+// block spans -- one builder's, or all of FinishTables' -- runs zero-copy,
+// hcrc_host_alloc), plain heap memory otherwise or when pinning fails.
+class HostBuf {
+ public:
+  HostBuf(bool pinned, size_t reserve) : pinned_(pinned) { Reserve(reserve); }
+  ~HostBuf() { Release(); }
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  void append(const char* p, size_t n) {
+    Reserve(size_ + n);
+    memcpy(data_ + size_, p, n);
+    size_ += n;
+  }
+  void append(const std::string& s) { append(s.data(), s.size()); }
+  char* data() { return data_; }
+  const char* data() const { return data_; }
+  size_t size() const { return size_; }
+  bool empty() const { return size_ == 0; }
+  void clear() { size_ = 0; }
+  char& operator[](size_t i) { return data_[i]; }
+
+ private:
+  void Reserve(size_t need) {
+    if (need <= cap_) return;
+    const size_t want = std::max(need, cap_ + cap_ / 2);
+    size_t cap = 0;
+    char* p = pinned_ ? PinnedPool::Get().Take(want, &cap) : nullptr;
+    const bool pinned = p != nullptr;
+    pinned_ = pinned;  // no pinned memory (no device): stop asking
+    if (!p) {
+      p = static_cast<char*>(malloc(want));
+      if (!p) throw std::bad_alloc();
+      cap = want;
+    }
+    if (size_) memcpy(p, data_, size_);
+    Release();
+    data_ = p;
+    cap_ = cap;
+    held_pinned_ = pinned;
+  }
+  void Release() {
+    if (!data_) return;
+    if (held_pinned_) PinnedPool::Get().Give(data_, cap_);
+    else free(data_);
+    data_ = nullptr;
+    cap_ = 0;
+  }
+  bool pinned_;
+  bool held_pinned_ = false;
+  char* data_ = nullptr;
+  size_t size_ = 0, cap_ = 0;
+};
+
+}  // namespace
+
 struct TableBuilder::Rep {
   TableOptions opt;
   const Comparator* cmp;
@@ -138,8 +248,8 @@ struct TableBuilder::Rep {
   std::unique_ptr<sst::FilterBuilder> filter;
   bool pending_index_entry = false;
   Handle pending_handle;
-  // bytes not yet handed to the sink; buf[0] is at file offset buf_start
-  std::string buf;
+  // bytes not yet handed to the sink
+  HostBuf buf;
   // blocks in buf whose trailer CRC is still to be computed:
   // (position of the contents in buf, contents size + 1 type byte)
   std::vector<std::pair<size_t, uint32_t>> pending;
@@ -150,7 +260,10 @@ struct TableBuilder::Rep {
         cmp(o.comparator ? o.comparator : BytewiseComparator()),
         sink(s),
         data_block(o.block_restart_interval),
-        index_block(1) {
+        index_block(1),
+        buf(o.pinned_buffers &&
+                (o.crc_mode == CrcMode::kBatchGpu || o.crc_mode == CrcMode::kBatchAuto),
+            o.max_buffer_size + (64u << 10)) {
     if (o.bloom_bits_per_key > 0) {
       filter.reset(new sst::FilterBuilder(o.bloom_bits_per_key));
       filter->StartBlock(0);

@@ -2,9 +2,13 @@
 // (SURVEY.md 8f-2): kv::ReadBlock (kv/src/table/format.cc:66-143) and
 // Table::Open / ReadMeta / ReadFilter with paranoid_checks plus a full
 // verified iteration (kv/src/table/table.cc:37-138), with every block CRC of
-// a stage computed in one batch (span_crc.h).
+// a stage computed in one batch (span_crc.h); and the compaction input path
+// (CompactionInput: MakeInputIteratorKV, kv/src/db/version_set.cc:1348-1373)
+// with its data blocks checked ahead of the merge, many per batch.
 #include <stdint.h>
 
+#include <algorithm>
+#include <queue>
 #include <string>
 #include <vector>
 
@@ -47,8 +51,10 @@ Status BlockValues(std::string_view b, std::vector<std::pair<std::string, std::s
   if (b.size() < 4) return Status::Corruption("bad block contents");
   const uint32_t nrest = sst::DecodeFixed32(b.data() + b.size() - 4);
   if (nrest > (b.size() - 4) / 4) return Status::Corruption("bad block contents");
+  if (nrest == 0) return Status::OK();  // an empty iterator (block.cc:261-262)
   const size_t limit_off = b.size() - (1 + size_t(nrest)) * 4;
-  const char* p = b.data();
+  // SeekToFirst: the first entry is at restart point 0 (block.cc SeekToRestartPoint)
+  const char* p = b.data() + sst::DecodeFixed32(b.data() + limit_off);
   const char* limit = b.data() + limit_off;
   std::string key;
   while (p < limit) {
@@ -263,6 +269,275 @@ Status VerifyTables(const char* const* images, const size_t* sizes, size_t n,
   }
   return first;
 }
+
+// ---------------------------------------------------------------------------
+// CompactionInput
+// ---------------------------------------------------------------------------
+namespace {
+
+// A block iterator's entries (kv/src/table/block.cc): decoded up to the end
+// or the first bad entry ("bad entry in block", the entries before it are
+// still returned), "bad block contents" for a block whose restart array
+// does not fit.
+Status BlockEntries(std::string_view b, std::vector<std::pair<std::string, std::string_view>>* kv) {
+  kv->clear();
+  return BlockValues(b, kv);
+}
+
+// Per-block state of the checks ahead of the merge.
+enum : uint8_t { kUnchecked = 0, kGood = 1, kBadCrc = 2, kShort = 3 };
+
+}  // namespace
+
+struct CompactionInput::Rep {
+  struct In {
+    const char* img;
+    size_t size;
+    Status open;                 // Table::Open's status
+    Status index;                // the index iterator's (bad entry in the index block)
+    Status saved;                // TwoLevelIterator::status_: the first block error
+    std::vector<Handle> blocks;  // data block handles, index order
+    std::vector<Status> bad_handle;  // per block: "bad block handle" (value undecodable)
+    std::vector<uint8_t> chk;    // per block: kUnchecked / kGood / kBadCrc / kShort
+    size_t next_check = 0;       // first block not yet sent to a CRC batch
+    size_t bi = 0;               // current block
+    std::vector<std::pair<std::string, std::string_view>> ents;
+    size_t ei = 0;
+    bool valid = false;
+    void Save(const Status& s) {
+      if (saved.ok() && !s.ok()) saved = s;
+    }
+    Status status() const {
+      if (!open.ok()) return open;
+      if (!index.ok()) return index;
+      return saved;
+    }
+  };
+  Options opt;
+  const Comparator* cmp;
+  std::vector<In> in;
+  uint64_t batches = 0, checked = 0;
+  Status fatal;  // a device error of a CRC batch (kBatchGpu)
+  // merge: the input holding the smallest key (ties: the lower input)
+  struct Later {
+    const Rep* r;
+    bool operator()(size_t a, size_t b) const {
+      const int c = r->cmp->Compare(r->in[a].ents[r->in[a].ei].first, r->in[b].ents[r->in[b].ei].first);
+      return c > 0 || (c == 0 && a > b);
+    }
+  };
+  std::priority_queue<size_t, std::vector<size_t>, Later> heap{Later{this}};
+  size_t cur = SIZE_MAX;
+
+  void Open() {
+    // Table::Open(paranoid_checks) of every input: one batch of index blocks
+    std::vector<TableJob> jobs(in.size());
+    std::vector<TableJob*> bt;
+    std::vector<Handle> bh;
+    for (size_t i = 0; i < in.size(); ++i) {
+      TableJob& j = jobs[i];
+      j.img = in[i].img;
+      j.size = in[i].size;
+      if (j.size < sst::kFooterLength) {
+        in[i].open = Status::Corruption("file is too short to be an sstable");
+        continue;
+      }
+      const char* f = j.img + j.size - sst::kFooterLength;
+      const uint64_t magic = uint64_t(sst::DecodeFixed32(f + sst::kFooterLength - 8)) |
+                             (uint64_t(sst::DecodeFixed32(f + sst::kFooterLength - 4)) << 32);
+      std::string_view fin(f, sst::kFooterLength);
+      if (magic != sst::kTableMagicNumber) {
+        in[i].open = Status::Corruption("not an sstable (bad magic number)");
+      } else if (!j.meta.DecodeFrom(&fin) || !j.index.DecodeFrom(&fin)) {
+        in[i].open = Status::Corruption("bad block handle");
+      } else if (!InBounds(j.size, j.index)) {
+        in[i].open = Status::Corruption("truncated block read");
+      } else {
+        bt.push_back(&j);
+        bh.push_back(j.index);
+      }
+    }
+    std::vector<bool> ok;
+    if (opt.verify_checksums && !bt.empty()) {
+      fatal = CheckBatch(bt, bh, opt.crc_mode, opt.device, &ok);
+      if (!fatal.ok()) return;
+      ++batches;
+      checked += bt.size();
+    }
+    for (size_t k = 0; k < bt.size(); ++k) {
+      In& x = in[static_cast<size_t>(bt[k] - jobs.data())];
+      const Handle& h = bh[k];
+      if (opt.verify_checksums && !ok[k]) {
+        x.open = Status::Corruption("block checksum mismatch");
+        continue;
+      }
+      x.open = TypeStatus(x.img, h);
+      if (!x.open.ok()) continue;
+      // the index iterator: handles up to a bad entry (the index's status)
+      std::vector<std::pair<std::string, std::string_view>> ents;
+      x.index = BlockEntries(std::string_view(x.img + h.offset, h.size), &ents);
+      for (auto& e : ents) {
+        Handle bhd;
+        std::string_view v = e.second;
+        const bool good = bhd.DecodeFrom(&v);
+        x.blocks.push_back(good ? bhd : Handle());
+        x.bad_handle.push_back(good ? Status::OK() : Status::Corruption("bad block handle"));
+      }
+      x.chk.assign(x.blocks.size(), kUnchecked);
+    }
+  }
+
+  // One CRC batch: the next prefetch_blocks unchecked blocks of every input
+  // that still has some (the merge drains the inputs at similar rates).
+  void CheckAhead() {
+    std::vector<TableJob> jobs;
+    std::vector<std::pair<size_t, size_t>> who;  // (input, block)
+    std::vector<TableJob*> bt;
+    std::vector<Handle> bh;
+    jobs.reserve(in.size());
+    for (size_t i = 0; i < in.size(); ++i) {
+      In& x = in[i];
+      if (!x.open.ok()) continue;
+      jobs.push_back(TableJob{});
+      jobs.back().img = x.img;
+      jobs.back().size = x.size;
+      const size_t end = std::min(x.blocks.size(), x.next_check + opt.prefetch_blocks);
+      for (size_t b = x.next_check; b < end; ++b) {
+        if (!x.bad_handle[b].ok()) continue;
+        if (!InBounds(x.size, x.blocks[b])) {
+          x.chk[b] = kShort;
+          continue;
+        }
+        who.emplace_back(i, b);
+        bt.push_back(&jobs.back());
+        bh.push_back(x.blocks[b]);
+      }
+      x.next_check = end;
+    }
+    if (bh.empty()) return;
+    std::vector<bool> ok;
+    fatal = CheckBatch(bt, bh, opt.crc_mode, opt.device, &ok);
+    if (!fatal.ok()) return;
+    ++batches;
+    checked += bh.size();
+    for (size_t k = 0; k < who.size(); ++k)
+      in[who[k].first].chk[who[k].second] = ok[k] ? kGood : kBadCrc;
+  }
+
+  // Table::BlockReader + the two-level iterator's skip of empty or failed
+  // blocks: position input x on block b or a later one with an entry.
+  void Load(In& x, size_t b) {
+    for (; b < x.blocks.size(); ++b) {
+      x.bi = b;
+      x.ents.clear();
+      x.ei = 0;
+      if (!x.bad_handle[b].ok()) {
+        x.Save(x.bad_handle[b]);
+        continue;
+      }
+      const Handle& h = x.blocks[b];
+      if (!InBounds(x.size, h)) {
+        x.Save(Status::Corruption("truncated block read"));
+        continue;
+      }
+      if (opt.verify_checksums) {
+        if (x.chk[b] == kUnchecked) CheckAhead();
+        if (!fatal.ok()) break;
+        if (x.chk[b] == kBadCrc) {
+          x.Save(Status::Corruption("block checksum mismatch"));
+          continue;
+        }
+      }
+      const Status ts = TypeStatus(x.img, h);
+      if (!ts.ok()) {
+        x.Save(ts);
+        continue;
+      }
+      x.Save(BlockEntries(std::string_view(x.img + h.offset, h.size), &x.ents));
+      if (!x.ents.empty()) {
+        x.valid = true;
+        return;
+      }
+    }
+    x.valid = false;
+  }
+
+  void Step(size_t i) {
+    In& x = in[i];
+    if (++x.ei < x.ents.size()) return;
+    Load(x, x.bi + 1);
+  }
+
+  void Pick() {
+    cur = SIZE_MAX;
+    if (!fatal.ok() || heap.empty()) return;
+    cur = heap.top();
+  }
+};
+
+CompactionInput::CompactionInput(const char* const* images, const size_t* sizes, size_t n,
+                                 const Options& o)
+    : rep_(new Rep) {
+  rep_->opt = o;
+  if (rep_->opt.prefetch_blocks == 0) rep_->opt.prefetch_blocks = 1;
+  rep_->cmp = o.comparator ? o.comparator : InternalBytewiseComparator();
+  rep_->in.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    rep_->in[i].img = images[i];
+    rep_->in[i].size = sizes[i];
+  }
+  rep_->Open();
+}
+
+CompactionInput::~CompactionInput() { delete rep_; }
+
+void CompactionInput::SeekToFirst() {
+  Rep* r = rep_;
+  r->heap = decltype(r->heap)(Rep::Later{r});
+  for (auto& x : r->in) {
+    x.saved = Status::OK();
+    x.valid = false;
+  }
+  if (!r->fatal.ok()) return;
+  for (size_t i = 0; i < r->in.size(); ++i) {
+    Rep::In& x = r->in[i];
+    if (!x.open.ok()) continue;
+    r->Load(x, 0);
+    if (x.valid) r->heap.push(i);
+  }
+  r->Pick();
+}
+
+bool CompactionInput::Valid() const { return rep_->cur != SIZE_MAX; }
+
+void CompactionInput::Next() {
+  Rep* r = rep_;
+  const size_t i = r->cur;
+  r->heap.pop();
+  r->Step(i);
+  if (r->in[i].valid) r->heap.push(i);
+  r->Pick();
+}
+
+std::string_view CompactionInput::key() const {
+  const Rep::In& x = rep_->in[rep_->cur];
+  return x.ents[x.ei].first;
+}
+
+std::string_view CompactionInput::value() const {
+  const Rep::In& x = rep_->in[rep_->cur];
+  return x.ents[x.ei].second;
+}
+
+Status CompactionInput::status() const {
+  if (!rep_->fatal.ok()) return rep_->fatal;
+  for (const auto& x : rep_->in)
+    if (!x.status().ok()) return x.status();
+  return Status::OK();
+}
+
+uint64_t CompactionInput::CrcBatches() const { return rep_->batches; }
+uint64_t CompactionInput::BlocksChecked() const { return rep_->checked; }
 
 }  // namespace table
 }  // namespace wipdb

@@ -93,6 +93,40 @@ int wsst_build_tables_ex(size_t ntables, const size_t* entries, const char* keys
   return Code(s);
 }
 
+int wsst_merge_tables(const char* const* images, const size_t* sizes, size_t n, int key_format,
+                      int verify, size_t prefetch_blocks, int crc_mode, int device,
+                      char* key_out, size_t key_cap, uint32_t* key_lens, char* val_out,
+                      size_t val_cap, uint32_t* val_lens, size_t max_entries,
+                      uint64_t* nentries, uint64_t* crc_batches) {
+  CrcMode mode;
+  if (!ModeOf(crc_mode, &mode) || (n && (!images || !sizes)) || !nentries ||
+      (key_format != WSST_KEYS_BYTEWISE && key_format != WSST_KEYS_INTERNAL))
+    return WSST_ERR_INVALID;
+  wipdb::table::CompactionInput::Options o;
+  o.comparator = key_format == WSST_KEYS_INTERNAL ? wipdb::table::InternalBytewiseComparator()
+                                                  : wipdb::table::BytewiseComparator();
+  o.verify_checksums = verify != 0;
+  o.prefetch_blocks = prefetch_blocks;
+  o.crc_mode = mode;
+  o.device = device;
+  wipdb::table::CompactionInput it(images, sizes, n, o);
+  size_t k = 0, ko = 0, vo = 0;
+  for (it.SeekToFirst(); it.Valid(); it.Next(), ++k) {
+    const std::string_view key = it.key(), val = it.value();
+    if (k >= max_entries || ko + key.size() > key_cap || vo + val.size() > val_cap)
+      return WSST_ERR_TOO_SMALL;
+    memcpy(key_out + ko, key.data(), key.size());
+    memcpy(val_out + vo, val.data(), val.size());
+    key_lens[k] = static_cast<uint32_t>(key.size());
+    val_lens[k] = static_cast<uint32_t>(val.size());
+    ko += key.size();
+    vo += val.size();
+  }
+  *nentries = k;
+  if (crc_batches) *crc_batches = it.CrcBatches();
+  return Code(it.status());
+}
+
 int wsst_read_block(const char* image, size_t n, uint64_t offset, uint64_t size) {
   if (!image) return WSST_ERR_INVALID;
   return Code(wipdb::table::ReadBlock(image, n, offset, size, true, nullptr));

@@ -39,6 +39,8 @@ _PROTOS = {
                                         _c.c_int, _sz, _c.c_int, _c.c_int, _c.c_int, _vp, _sz,
                                         _vp, _vp, _vp]),
     "wsst_read_block": (_c.c_int, [_vp, _sz, _c.c_uint64, _c.c_uint64]),
+    "wsst_merge_tables": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_int, _sz, _c.c_int, _c.c_int,
+                                     _vp, _sz, _vp, _vp, _sz, _vp, _sz, _vp, _vp]),
     "wsst_verify_tables": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_int, _c.c_int, _vp, _vp,
                                       _vp]),
     "wsst_log_write": (_c.c_int, [_vp, _vp, _sz, _c.c_int, _c.c_uint64, _c.c_int, _c.c_int, _vp,
@@ -129,11 +131,21 @@ def build_tables_raw(entries, keys: bytes, klen, vals: bytes, vlen, block_size: 
 def verify_tables(images: Sequence[bytes], bloom_bits: int = 0, crc_mode: int = CRC_BATCH_AUTO,
                   device: int = 0, count_blocks: bool = False):
     """Returns (first status code, per-table codes[, blocks checked, bad blocks])."""
-    lib = _load()
-    n = len(images)
     bufs = [_c.create_string_buffer(im, len(im) or 1) for im in images]
-    ptrs = (_c.c_void_p * max(n, 1))(*[_c.addressof(b) for b in bufs])
-    sizes = np.array([len(im) for im in images] or [0], dtype=np.uint64)
+    return verify_tables_at([_c.addressof(b) for b in bufs], [len(im) for im in images],
+                            bloom_bits, crc_mode, device, count_blocks)
+
+
+def verify_tables_at(addrs: Sequence[int], sizes: Sequence[int], bloom_bits: int = 0,
+                     crc_mode: int = CRC_BATCH_AUTO, device: int = 0,
+                     count_blocks: bool = False):
+    """verify_tables over images already in memory at the given addresses
+    (e.g. in pinned memory from PinnedImages, which the MI355X reads
+    zero-copy)."""
+    lib = _load()
+    n = len(addrs)
+    ptrs = (_c.c_void_p * max(n, 1))(*addrs)
+    sizes = np.array(list(sizes) or [0], dtype=np.uint64)
     codes = np.zeros(max(n, 1), np.int32)
     chk, bad = _c.c_uint64(0), _c.c_uint64(0)
     global last_call_seconds
@@ -147,6 +159,71 @@ def verify_tables(images: Sequence[bytes], bloom_bits: int = 0, crc_mode: int = 
     if count_blocks:
         return rc, codes[:n].tolist(), int(chk.value), int(bad.value)
     return rc, codes[:n].tolist()
+
+
+def merge_tables(images: Sequence[bytes], key_format: int = KEYS_INTERNAL, verify: bool = True,
+                 prefetch_blocks: int = 64, crc_mode: int = CRC_BATCH_AUTO, device: int = 0):
+    """The compaction input path (MakeInputIteratorKV): the merged entries of
+    the tables, data blocks checked ahead of the merge in batches.  Returns
+    (status code, [(key, value), ...], CRC batches issued)."""
+    lib = _load()
+    n = len(images)
+    bufs = [_c.create_string_buffer(im, len(im) or 1) for im in images]
+    ptrs = (_c.c_void_p * max(n, 1))(*[_c.addressof(b) for b in bufs])
+    sizes = np.array([len(im) for im in images] or [0], dtype=np.uint64)
+    cap = sum(len(im) for im in images) * 4 + 4096
+    kout, vout = _c.create_string_buffer(cap), _c.create_string_buffer(cap)
+    maxe = cap // 4
+    kl, vl = np.zeros(maxe, np.uint32), np.zeros(maxe, np.uint32)
+    ne, nb = _c.c_uint64(0), _c.c_uint64(0)
+    global last_call_seconds
+    t0 = time.perf_counter()
+    rc = lib.wsst_merge_tables(ptrs, sizes.ctypes.data, n, key_format, int(verify),
+                               prefetch_blocks, crc_mode, device, kout, cap, kl.ctypes.data,
+                               vout, cap, vl.ctypes.data, maxe, _c.byref(ne), _c.byref(nb))
+    last_call_seconds = time.perf_counter() - t0
+    if rc < 0:
+        raise SstError(f"wsst_merge_tables: {rc}")
+    k, v = kout.raw, vout.raw
+    out, ko, vo = [], 0, 0
+    for i in range(int(ne.value)):
+        out.append((k[ko:ko + int(kl[i])], v[vo:vo + int(vl[i])]))
+        ko += int(kl[i])
+        vo += int(vl[i])
+    return rc, out, int(nb.value)
+
+
+class PinnedImages:
+    """Table images copied into one pinned host allocation (hcrc_host_alloc),
+    the way a store would keep SST pages it checksums often: hcrc_batch
+    reads spans there zero-copy over PCIe instead of staging them."""
+
+    def __init__(self, images: Sequence[bytes]):
+        from wipdb_amd import _lib as hl
+        self._hl = hl.load()
+        total = sum(len(i) for i in images) + 64 * len(images) + 64
+        ptr = _c.c_void_p()
+        hl.check(self._hl.hcrc_host_alloc(total, _c.byref(ptr)), "hcrc_host_alloc")
+        self.ptr = ptr.value
+        self.addrs, self.sizes = [], []
+        at = self.ptr
+        for im in images:
+            _c.memmove(at, im, len(im))
+            self.addrs.append(at)
+            self.sizes.append(len(im))
+            at += (len(im) + 63) // 64 * 64
+        self.nbytes = sum(self.sizes)
+
+    def close(self):
+        if self.ptr:
+            self._hl.hcrc_host_free(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def read_block(image: bytes, offset: int, size: int) -> int:
