@@ -92,3 +92,22 @@ def test_kernel_span_geometry_host(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "PASS" in r.stdout
+
+
+def test_host_code_under_sanitizers():
+    """the library's host code (CPU CRC path, table / log layers,
+    compaction input, C-ABI checks) built with -fsanitize=address,undefined
+    (make -C wipdb_amd/csrc sanitize) runs clean over clean and damaged
+    inputs (tests/cpp/test_host_sanitize.cc)."""
+    from tests.conftest import gpu_available
+    if gpu_available():
+        pytest.skip("host-only check; run on the CPU container")
+    env = dict(os.environ, PYTORCH_ROCM_ARCH="gfx950")
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "wipdb_amd", "csrc"), "sanitize",
+                    "ARCH=gfx950"], check=True, env=env, timeout=900)
+    exe = os.path.join(REPO, "build", "sanitize", "test_host_sanitize")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+                                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    assert "PASS" in r.stdout
