@@ -7,7 +7,11 @@ line per workload.  Times are the native C-ABI call alone (sst.last_call_seconds
               together: table MB/s for kInline (the reference's schedule:
               CRC per block on the host), kBatchCpu, kBatchGpu.
   verify      the same tables through the batched Table::Open + verified
-              iteration: MB/s per schedule.
+              iteration: MB/s per schedule (and, on the MI355X, with the
+              images in pinned memory: zero-copy).
+  merge       the compaction input path (MakeInputIteratorKV): the merged
+              entries of the same tables read with paranoid checks, data
+              blocks checked 64 per input per CRC batch: MB/s per schedule.
   wal         a log of R WriteBatch-sized records (100-400 B): AddRecord
               layout + CRCs (write) and the recovery read, MB/s per schedule.
 
@@ -94,6 +98,21 @@ def main():
             res["batch_gpu_pinned_images"] = {"s": round(t, 4),
                                               "MB_per_s": round(pin.nbytes / 1e6 / t, 1)}
     print(json.dumps(res), flush=True)
+
+    res = {"workload": "merge", "tables": len(imgs_ref)}
+    want = None
+    for m in modes:
+        t, (rc, ents, batches) = best(lambda: sst.merge_tables(
+            imgs_ref, key_format=sst.KEYS_BYTEWISE, prefetch_blocks=64, crc_mode=MODES[m]), a.reps)
+        assert rc == sst.OK
+        if want is None:
+            want = ents
+        assert ents == want, f"{m}: merged entries differ between CRC schedules"
+        res[m] = {"s": round(t, 4), "MB_per_s": round(sum(len(i) for i in imgs_ref) / 1e6 / t, 1),
+                  "crc_batches": batches}
+    res["entries"] = len(want)
+    print(json.dumps(res), flush=True)
+    del want
 
     rng = np.random.default_rng(2)
     lens = rng.integers(100, 400, size=a.records)
