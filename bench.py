@@ -287,7 +287,13 @@ def main():
         total_bytes = world * nblk * BLOCK
         value = total_bytes * a.steps / elapsed_max / 2**30
         achieved = nblk * ALGO_BYTES_PER_BLOCK / (kern_avg_ms * 1e-3) / 1e9
-        cfg = "BASELINE configs[1]" if world == 1 else "BASELINE configs[3]: 8 M blocks per GPU"
+        if nblk == 1 << 20 and world == 1:
+            cfg = "BASELINE configs[1]"
+        elif nblk == 8 << 20:
+            cfg = "BASELINE configs[3]: its 8 M-block per-GPU shard" + (
+                " (one GPU)" if world == 1 else "")
+        else:
+            cfg = "custom size (--blocks)"
         line = {
             "metric": "device-resident GiB/s, batched CRC32C of 4 KiB blocks, 1/2/4/8 MI355X",
             "value": round(value, 2),

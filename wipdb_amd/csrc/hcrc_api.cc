@@ -402,16 +402,19 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
 }
 
 // Whether a host piece should go through the size classes: enough spans of
-// at most 2 KiB (WAL records, small meta blocks) to pay for the partition
-// pass and the two extra launches (table blocks -- 4 KiB plus their last
-// entry -- need no classes: the spans kernel batches their front pieces).
+// at most ~1.25 KiB (WAL records, small meta blocks) to pay for the
+// partition pass and the two extra launches.  Larger spans run as fast or
+// faster on the spans kernel (config 3, profiles/r02d_extra*.log: 2 KiB
+// spans 3186 GiB/s unsplit vs 2891 split; 1 KiB spans 1592 vs 2602), and
+// table blocks -- 4 KiB plus their last entry -- need no classes at all.
 // Span i's address mod 16 is base + offsets[i]'s.
 constexpr size_t kAutoSplitMin = 256;
+constexpr uint32_t kAutoSplitChunks = 80;
 int AutoSplit(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, size_t n) {
   size_t hits = 0;
   for (size_t i = 0; i < n && hits < kAutoSplitMin; ++i) {
     const uint32_t h = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(base) + offsets[i]) & 15u);
-    hits += ((h + lengths[i]) >> 4) <= lk::kClass2Chunks;
+    hits += ((h + lengths[i]) >> 4) <= kAutoSplitChunks;
   }
   return hits >= kAutoSplitMin ? HCRC_SPLIT_SMALL : 0;
 }
