@@ -128,10 +128,22 @@ struct Case {
       if (fl & kEMain) {
         const uint32_t hp = g.c.php(), r = g.c.r();
         const uint32_t pw = g.c.piece_word();
-        const uint32_t Tm = verify ? R ^ stored_x : R;
+        if ((fl & kEAux) || r > kPieceMax) {
+          fprintf(stderr, "  piece span with an aux chunk in its main segment / too long\n");
+          ++g_fail;
+        }
         uint8_t pwin[256];
-        for (uint32_t t = 0; t < kPieceChunks; ++t)
-          memcpy(pwin + 16 * t, Read(sbase + g.c.c0 + PieceChunkOffset(pw, t), 16), 16);
+        for (uint32_t t = 0; t < kPieceChunks; ++t) {
+          const uint64_t at = sbase + g.c.c0 + PieceChunkOffset(pw, t, verify);
+          if (t == 0u && (at & 3u)) {
+            fprintf(stderr, "  piece aux chunk not dword aligned\n");
+            ++g_fail;
+          }
+          memcpy(pwin + 16 * t, Read(at, 16), 16);
+        }
+        // window chunk 0: the aux chunk (tail word, trailer)
+        const uint32_t tw = Le32(pwin + PieceTailAt(pw, verify));
+        const uint32_t stored_p = verify ? ~Unmask(Le32(pwin + PieceTrailerAt(pw))) : 0u;
         const uint32_t front = kPieceChunks - r;
         memset(pwin, 0, 16 * front);
         uint32_t c[4];
@@ -139,8 +151,11 @@ struct Case {
         fix_head(c, hp, g.c.pws(), HeadRegister(init, hp));
         memcpy(pwin + 16 * front, c, 16);
         const uint32_t rp = Feed(0u, pwin, sizeof(pwin));
-        const uint32_t v = FeedZeros(rp, 4096u + g.c.k()) ^ Tm;
-        result = verify ? (v == 0u) : ~v;
+        uint32_t v = FeedZeros(rp, 4096u) ^ R;  // the register after piece || main
+        uint8_t t4[4];
+        memcpy(t4, &tw, 4);
+        v = Feed(v, t4, g.c.k());                 // the tail
+        result = verify ? (v == stored_p) : ~v;
         break;
       } else if (fl & kELast) {
         result = verify ? (R == stored_x) : ~R;
@@ -164,7 +179,7 @@ void Check(std::vector<uint8_t>& buf, uint64_t sbase, uint64_t s_abs, uint32_t n
         SpanD d{s_abs - sbase, n, init, 0u, 7u};
         WalkE wk;
         wk.start(sbase, d, false);
-        fprintf(stderr, "F geo %x nseg %u nc0 %u pg %u\n", wk.geo, wk.nseg, wk.nc0, unsigned(s_abs & 4095));
+        fprintf(stderr, "F geo %x nseg %u nc0 %u pg %u\n", wk.geo, wk.nseg, wk.geo >> 18, unsigned(s_abs & 4095));
       }
       if (g_fail < 20)
         fprintf(stderr, "crc  s %#llx n %u init %#x: got %08x want %08x\n",

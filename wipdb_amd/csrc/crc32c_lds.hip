@@ -660,7 +660,7 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       const uint64_t c0 = (static_cast<uint64_t>(bperm(ring.a_hi, idx)) << 32) | bperm(ring.a_lo, idx);
       const uint32_t pw = bperm(ring.pw, idx);
       // lane m of the quarter loads window chunk cm mod 16 of its piece
-      if (p < n) dma1v(sbase + c0 + PieceChunkOffset(pw, pp.cm & 15u), pp.slot + 1024u * q);
+      if (p < n) dma1v(sbase + c0 + PieceChunkOffset(pw, pp.cm & 15u, kVerify), pp.slot + 1024u * q);
     }
   };
 
@@ -723,6 +723,11 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       const uint32_t T = bperm(ring.T, idx), sid = bperm(ring.id, idx);
       const int32_t front = static_cast<int32_t>(kPieceChunks - (on ? pw & 63u : 0u));
       const uint32_t hp = (pw >> 8) & 15u, ws = (pw >> 12) & 3u, k = (pw >> 14) & 3u;
+      // window chunk 0 (the group leader's first chunk) is the span's aux
+      // chunk: its tail word and stored trailer
+      const u32x4 axc{W[0], W[1], W[2], W[3]};
+      const uint32_t tw = le32_at(axc, u32x4{0, 0, 0, 0}, PieceTailAt(pw, kVerify));
+      const uint32_t tv = kVerify ? ~unmask_crc(le32_at(axc, u32x4{0, 0, 0, 0}, PieceTrailerAt(pw))) : 0u;
       // zero the chunks in front of the piece; its chunk 0 into span form
       uint32_t c[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -743,10 +748,11 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       }
       const uint32_t rp = fold4(lk, l, scan(lk, W));
       if (gl == 0u && on) {
-        // register of the whole span = rp * x^(8 (4096 + k)) ^ main register
+        // register after piece || main = rp * x^(8 * 4096) ^ main register;
+        // then the tail
         const uint32_t sft = l2_shift(lk, make_l2c(l, 1u), l2_shift(lk, make_l2c(l, 7u), rp));
-        const uint32_t v = tail_step(lk, sft, 0u, k) ^ T;
-        if (kVerify) out8[sid] = v == 0u ? 1u : 0u;
+        const uint32_t v = tail_step(lk, sft ^ T, tw, k);
+        if (kVerify) out8[sid] = v == tv ? 1u : 0u;
         else out32[sid] = msk ? mask_crc(~v) : ~v;
       }
       did_store = true;
@@ -774,10 +780,10 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       }
       if (fl & kEMain) {
         // the front piece goes to the ring with its head register; the span
-        // is finished there: rp * x^(8 (4096 + k)) ^ T (== 0 <=> a good block)
+        // (its tail, its trailer) is finished there
         const uint32_t pw = cur.piece_word();
         const uint32_t hin = head_register(l, cur.init, cur.php());
-        ring.push(l, cur.c0, pw, hin, kVerify ? R ^ stored_x : R, cur.id);
+        ring.push(l, cur.c0, pw, hin, R, cur.id);
       } else if (fl & kELast) {
         did_store = true;
         if (l == 0u) {

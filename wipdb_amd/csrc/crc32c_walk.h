@@ -60,7 +60,8 @@ WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {
 // ---------------------------------------------------------------------------
 constexpr uint32_t kEValid = 1u, kEFirst = 2u, kELast = 4u, kEMain = 8u, kEBatch = 16u,
                    kENoBody = 32u, kEAux = 64u;
-constexpr uint32_t kPieceChunks = 16;  // a piece: 4 lanes x 4 chunks
+constexpr uint32_t kPieceChunks = 16;  // a piece window: 4 lanes x 4 chunks
+constexpr uint32_t kPieceMax = 15;     // piece chunks: window chunk 0 stays free for the aux chunk
 constexpr uint32_t kBatch = 16;        // pieces per batch iteration
 
 // A segment as issued (DMA sources) and as computed (the packed SegC, the
@@ -96,10 +97,12 @@ struct SegE {
 };
 
 struct WalkE {
-  uint64_t c0, ax;
+  uint64_t c0;
+  uint32_t axd;   // the aux chunk at c0 + (int32) axd
   uint32_t id, init;
-  uint32_t geo;   // hp | ws << 4 | k << 6 | te << 8 | tv << 12 | piece << 16
-  uint32_t nc0;   // chunks of the first segment (piece: the piece's)
+  // hp | ws << 4 | k << 6 | te << 8 | tv << 12 | piece << 16 | no body << 17 |
+  // nc0 << 18 (chunks of the first segment; piece: the piece's)
+  uint32_t geo;
   uint32_t j, nseg;
   bool valid;
 
@@ -127,11 +130,12 @@ struct WalkE {
     // reading hp bytes in front of s would leave its page: read chunk 0 from
     // s rounded down to 4, i.e. ws = (hp - s % 4) / 4 words late
     if (pg < hp) geo |= ((hp - (pg & 3u)) >> 2) << 4;
+    uint32_t nc0;
     if (C <= kSegChunks) {
       nseg = 1;
       nc0 = C;
       if (C == 0u) geo |= 1u << 17;
-    } else if (C <= kSegChunks + kPieceChunks) {
+    } else if (C <= kSegChunks + kPieceMax) {
       nseg = 1;
       nc0 = C - kSegChunks;
       geo |= 1u << 16;
@@ -139,6 +143,7 @@ struct WalkE {
       nseg = (C + kSegChunks - 1u) / kSegChunks;
       nc0 = C - kSegChunks * (nseg - 1u);
     }
+    geo |= nc0 << 18;
     if (verify || k != 0u) {
       // the aux chunk: 16 bytes ending at the 4-byte word that holds the
       // span's last byte (verify: the trailer's last byte) -- or, when they
@@ -147,25 +152,27 @@ struct WalkE {
       const uint32_t a_lo = ((need + 3u) & ~3u) - 16u;  // 16 <= n + 7: a_lo may precede s
       const uint32_t before = s_lo - a_lo;              // bytes in front of s (mod 2^32)
       const uint32_t a_fix = (before <= 16u && before > pg) ? (s_lo & ~3u) : a_lo;
-      ax = d.a + static_cast<uint64_t>(static_cast<int32_t>(a_fix - s_lo));
+      axd = (a_fix - s_lo) + hp;  // from c0 = s - hp
       const uint32_t te = (e_lo - k - a_fix) & 15u;
       const uint32_t tv = (e_lo - a_fix) & 15u;
       geo |= (te << 8) | (tv << 12);
     } else {
-      ax = 0;
+      axd = 0;
     }
   }
   WIPDB_LK_HD inline SegE next(bool verify) {
     SegE g;
     const bool last = j + 1u == nseg;
     const uint32_t hp = geo & 15u, ws = (geo >> 4) & 3u, k = (geo >> 6) & 3u;
+    const uint32_t nc0 = geo >> 18;
     uint32_t fl = kEValid | (last ? kELast : 0u);
-    if (last && (verify || k != 0u)) fl |= kEAux;
+    // (a piece span's tail word / trailer come with its piece, PieceChunkOffset)
+    if (last && (verify || k != 0u) && !(geo & (1u << 16))) fl |= kEAux;
     g.c.init = init;
     g.c.id = id;
     g.c.c0 = c0;
     g.c.g2 = (geo >> 12) & 15u;
-    g.ax = ax;
+    g.ax = c0 + static_cast<uint64_t>(static_cast<int64_t>(static_cast<int32_t>(axd)));
     g.src0 = 0;
     uint32_t front = 0, h = 0, w = 0;
     if (geo & (3u << 16)) {
@@ -204,7 +211,21 @@ WIPDB_LK_HD inline uint32_t SegChunkOffset(const SegE& g, uint32_t t) {
 
 // The DMA source of window chunk t (0..15) of a front piece with ring word
 // pw (chunks | hp << 8 | ws << 12 | k << 14), from sbase + its c0.
-WIPDB_LK_HD inline uint32_t PieceChunkOffset(uint32_t pw, uint32_t t) {
+// Window chunk 0 (always in front of a piece of <= kPieceMax chunks) instead
+// reads the span's aux chunk: the 16 bytes ending at the 4-byte word holding
+// its last byte (verify: its trailer's last byte), i.e. at offset
+// 16 (C - 1) + 4 verify + 4 [k > 0] from chunk 0, C = 256 + piece chunks;
+// the tail word is at byte PieceTailAt, the trailer at PieceTrailerAt.
+WIPDB_LK_HD inline uint32_t PieceAuxOffset(uint32_t pw, bool verify) {
+  const uint32_t k = (pw >> 14) & 3u;
+  return 16u * (kSegChunks + (pw & 63u) - 1u) + (verify ? 4u : 0u) + (k != 0u ? 4u : 0u);
+}
+WIPDB_LK_HD inline uint32_t PieceTailAt(uint32_t pw, bool verify) {
+  return 16u - (verify ? 4u : 0u) - (((pw >> 14) & 3u) != 0u ? 4u : 0u);
+}
+WIPDB_LK_HD inline uint32_t PieceTrailerAt(uint32_t pw) { return PieceTailAt(pw, true) + ((pw >> 14) & 3u); }
+WIPDB_LK_HD inline uint32_t PieceChunkOffset(uint32_t pw, uint32_t t, bool verify) {
+  if (t == 0u) return PieceAuxOffset(pw, verify);
   const int32_t front = static_cast<int32_t>(kPieceChunks - (pw & 63u));
   const int32_t s0 = static_cast<int32_t>(4u * ((pw >> 12) & 3u));
   const int32_t b = 16 * (static_cast<int32_t>(t) - front);
