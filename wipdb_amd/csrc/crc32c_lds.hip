@@ -660,7 +660,7 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       const uint64_t c0 = (static_cast<uint64_t>(bperm(ring.a_hi, idx)) << 32) | bperm(ring.a_lo, idx);
       const uint32_t pw = bperm(ring.pw, idx);
       // lane m of the quarter loads window chunk cm mod 16 of its piece
-      if (p < n) dma1v(sbase + c0 + PieceChunkOffset(pw, pp.cm & 15u, kVerify), pp.slot + 1024u * q);
+      if (p < n) dma1v(sbase + c0 + PieceChunkOffset(pw, pp.cm & 15u), pp.slot + 1024u * q);
     }
   };
 
@@ -672,7 +672,7 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
   prefetch(pf);
   SegC cur;
   {
-    const SegE g = wk.next(kVerify);
+    const SegE g = wk.next();
     issue(g);
     cur = g.c;
   }
@@ -708,7 +708,7 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
         wk.start(sbase, pf.d, kVerify);
         took_pf = true;
       }
-      const SegE g = wk.next(kVerify);
+      const SegE g = wk.next();
       issue(g);
       nxt = g.c;
     }
@@ -724,10 +724,8 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       const int32_t front = static_cast<int32_t>(kPieceChunks - (on ? pw & 63u : 0u));
       const uint32_t hp = (pw >> 8) & 15u, ws = (pw >> 12) & 3u, k = (pw >> 14) & 3u;
       // window chunk 0 (the group leader's first chunk) is the span's aux
-      // chunk: its tail word and stored trailer
-      const u32x4 axc{W[0], W[1], W[2], W[3]};
-      const uint32_t tw = le32_at(axc, u32x4{0, 0, 0, 0}, PieceTailAt(pw, kVerify));
-      const uint32_t tv = kVerify ? ~unmask_crc(le32_at(axc, u32x4{0, 0, 0, 0}, PieceTrailerAt(pw))) : 0u;
+      // chunk: its tail word is the last word
+      const uint32_t tw = W[3];
       // zero the chunks in front of the piece; its chunk 0 into span form
       uint32_t c[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -750,10 +748,14 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       if (gl == 0u && on) {
         // register after piece || main = rp * x^(8 * 4096) ^ main register;
         // then the tail
+        // (verify: T holds the residue, and there is no tail)
         const uint32_t sft = l2_shift(lk, make_l2c(l, 1u), l2_shift(lk, make_l2c(l, 7u), rp));
-        const uint32_t v = tail_step(lk, sft ^ T, tw, k);
-        if (kVerify) out8[sid] = v == tv ? 1u : 0u;
-        else out32[sid] = msk ? mask_crc(~v) : ~v;
+        if (kVerify) {
+          out8[sid] = sft == T ? 1u : 0u;
+        } else {
+          const uint32_t v = tail_step(lk, sft ^ T, tw, k);
+          out32[sid] = msk ? mask_crc(~v) : ~v;
+        }
       }
       did_store = true;
     } else {
@@ -770,24 +772,34 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
         } else {
           prepare_first(W, l, cur.front(), cur.hp(), cur.ws(), inj);
         }
+        if (kVerify && (fl & kELast)) {
+          // the stored trailer, unmasked in place (lane 63, words 14-15)
+          uint32_t lo = W[14], hi = W[15];
+          fix_trailer(lo, hi, cur.jv());
+          W[14] = l == 63u ? lo : W[14];
+          W[15] = l == 63u ? hi : W[15];
+        }
         R = fold<1>(lk, l, scan(lk, W))[0];
       }
-      uint32_t stored_x = 0;  // verify: ~Unmask(the stored crc)
       if (fl & kEAux) {
         const u32x4 a{uni(ax.x), uni(ax.y), uni(ax.z), uni(ax.w)};
-        if (cur.k() != 0u) R = uni(tail_step(lk, R, le32_at(a, u32x4{0, 0, 0, 0}, cur.te()), cur.k()));
-        if (kVerify) stored_x = ~unmask_crc(le32_at(a, u32x4{0, 0, 0, 0}, cur.tv()));
+        R = uni(tail_step(lk, R, le32_at(a, u32x4{0, 0, 0, 0}, cur.te()), cur.k()));
       }
+      // verify: a good block leaves the residue
+      constexpr uint32_t kRes0 = verify_residue(0), kRes1 = verify_residue(1),
+                         kRes2 = verify_residue(2), kRes3 = verify_residue(3);
+      const uint32_t jv = cur.jv();
+      const uint32_t res = jv == 0u ? kRes0 : (jv == 1u ? kRes1 : (jv == 2u ? kRes2 : kRes3));
       if (fl & kEMain) {
         // the front piece goes to the ring with its head register; the span
-        // (its tail, its trailer) is finished there
+        // (its tail) is finished there
         const uint32_t pw = cur.piece_word();
         const uint32_t hin = head_register(l, cur.init, cur.php());
-        ring.push(l, cur.c0, pw, hin, R, cur.id);
+        ring.push(l, cur.c0, pw, hin, kVerify ? R ^ res : R, cur.id);
       } else if (fl & kELast) {
         did_store = true;
         if (l == 0u) {
-          if (kVerify) out8[cur.id] = R == stored_x ? 1u : 0u;
+          if (kVerify) out8[cur.id] = R == res ? 1u : 0u;
           else out32[cur.id] = msk ? mask_crc(~R) : ~R;
         }
       } else {

@@ -42,21 +42,23 @@ WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {
 // below s, chunk 0 is read from s rounded down to 4 and shifted right by whole
 // words before the mask.  The tail is ONE slicing step:
 //   reg' = T-step((reg ^ tail word) << 8 (4 - k)) ^ (reg >> 8 k),
-// with the tail word (and a verify span's stored trailer) in 16 bytes read
-// with the last segment.  Nothing outside [s, E) (+ the 4 trailer bytes of a
-// verify span) is read, except within the 4-byte words holding s and E.
+// with the tail word in 16 bytes read with the last segment.  A verify span
+// has no tail: its grid runs on over the 4-byte stored trailer to the next
+// 4-byte boundary, and the trailer is checked through the CRC residue
+// (fix_trailer).  Nothing outside [s, E) (+ the trailer of a verify span) is
+// read, except within the 4-byte words holding s and E.
 //
 // Segments are 256-chunk windows END-aligned at their last chunk: the first
 // covers chunks [0, C - 256 (m - 1)), the m - 1 others 256 each, chained by
-// the register.  A span of 257..288 chunks (a table block: 4 KiB + its last
+// the register.  A span of 257..271 chunks (a table block: 4 KiB + its last
 // entry + the type byte) is instead ONE full main segment -- its last 256
-// chunks and its tail, from a zero register -- plus a front piece of its first
-// 1..16 chunks, which joins the wave's piece ring: entry k in lane k of six
+// chunks, from a zero register -- plus a front piece of its first 1..15
+// chunks, which joins the wave's piece ring: entry k in lane k of six
 // VGPRs.  Once 16 are pending (or the wave runs out of segments), one
 // iteration CRCs them all, a piece per 4-lane group (a 16-chunk window each,
 // four per DMA instruction with per-lane addresses), folded within the group
 // (level 1 + DPP), and finishes each span by linearity:
-//   register = piece register * x^(8 (4096 + k)) ^ main register.
+//   register = piece register * x^(8 * 4096) ^ main register, then the tail.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kEValid = 1u, kEFirst = 2u, kELast = 4u, kEMain = 8u, kEBatch = 16u,
                    kENoBody = 32u, kEAux = 64u;
@@ -69,7 +71,7 @@ constexpr uint32_t kBatch = 16;        // pieces per batch iteration
 // resource).
 //   g1: flags (8) | front (9) << 8 | hp (4) << 17 | ws (2) << 21 | k (2) << 23 |
 //       te (4) << 25
-//   g2: tv (4) | main: the front piece's chunks (5) << 4 | its hp (4) << 9 |
+//   g2: jv (2) | main: the front piece's chunks (5) << 4 | its hp (4) << 9 |
 //       its ws (2) << 13
 struct SegC {
   uint32_t g1, g2;
@@ -82,7 +84,7 @@ struct SegC {
   WIPDB_LK_HD inline uint32_t ws() const { return (g1 >> 21) & 3u; }
   WIPDB_LK_HD inline uint32_t k() const { return (g1 >> 23) & 3u; }
   WIPDB_LK_HD inline uint32_t te() const { return (g1 >> 25) & 15u; }
-  WIPDB_LK_HD inline uint32_t tv() const { return g2 & 15u; }
+  WIPDB_LK_HD inline uint32_t jv() const { return g2 & 3u; }  // verify: grid bytes past the trailer
   WIPDB_LK_HD inline uint32_t r() const { return (g2 >> 4) & 31u; }
   WIPDB_LK_HD inline uint32_t php() const { return (g2 >> 9) & 15u; }
   WIPDB_LK_HD inline uint32_t pws() const { return (g2 >> 13) & 3u; }
@@ -92,7 +94,7 @@ struct SegC {
 struct SegE {
   SegC c;
   uint64_t wb;    // offset (from the source base) of window chunk 0
-  uint64_t ax;    // last: offset of the 16 bytes holding the tail word / verify trailer
+  uint64_t ax;    // last: offset of the 16 bytes holding the tail word
   uint32_t src0;  // DMA offset (from wb) of the span's chunk 0, also read by the in-front lanes
 };
 
@@ -100,24 +102,33 @@ struct WalkE {
   uint64_t c0;
   uint32_t axd;   // the aux chunk at c0 + (int32) axd
   uint32_t id, init;
-  // hp | ws << 4 | k << 6 | te << 8 | tv << 12 | piece << 16 | no body << 17 |
+  // hp | ws << 4 | k << 6 | te << 8 | jv << 12 | piece << 16 | no body << 17 |
   // nc0 << 18 (chunks of the first segment; piece: the piece's)
   uint32_t geo;
   uint32_t j, nseg;
   bool valid;
 
   // sbase: the source base address; verify: the span is followed by a
-  // 4-byte trailer that the last segment reads.  Scalar work per span is the
+  // 4-byte trailer, which the grid takes in.  Scalar work per span is the
   // kernels' scarce resource (one scalar unit per CU serves 16 waves): the
   // rare parts -- the aux chunk, a head read late, pieces, several segments
   // -- sit behind uniform branches.
   WIPDB_LK_HD inline void start(uint64_t sbase, const SpanD& d, bool verify) {
     const uint32_t n = d.n;
     const uint32_t s_lo = static_cast<uint32_t>(sbase) + static_cast<uint32_t>(d.a);
-    const uint32_t e_lo = s_lo + n;
-    const uint32_t e3 = e_lo & 3u;
-    const uint32_t k = e3 < n ? e3 : n;  // tail bytes
-    const uint32_t nb = n - k;           // body bytes [s, E4)
+    uint32_t k, nb, jv = 0;
+    if (verify) {
+      // the grid takes the stored trailer and ends at the first 4-byte
+      // boundary at or after it: jv <= 3 bytes past it, in its last word
+      const uint32_t e_lo = s_lo + n + 4u;
+      jv = (0u - e_lo) & 3u;
+      k = 0;
+      nb = n + 4u + jv;
+    } else {
+      const uint32_t e3 = (s_lo + n) & 3u;
+      k = e3 < n ? e3 : n;  // tail bytes
+      nb = n - k;           // body bytes [s, E4)
+    }
     const uint32_t C = (nb + 15u) >> 4;
     const uint32_t hp = (C << 4) - nb;
     c0 = d.a - hp;
@@ -125,7 +136,7 @@ struct WalkE {
     id = static_cast<uint32_t>(d.id);
     j = 0;
     valid = true;
-    geo = hp | (k << 6);
+    geo = hp | (k << 6) | (jv << 12);
     const uint32_t pg = s_lo & 4095u;
     // reading hp bytes in front of s would leave its page: read chunk 0 from
     // s rounded down to 4, i.e. ws = (hp - s % 4) / 4 words late
@@ -144,34 +155,32 @@ struct WalkE {
       nc0 = C - kSegChunks * (nseg - 1u);
     }
     geo |= nc0 << 18;
-    if (verify || k != 0u) {
+    if (k != 0u) {
       // the aux chunk: 16 bytes ending at the 4-byte word that holds the
-      // span's last byte (verify: the trailer's last byte) -- or, when they
-      // would start in the page below a short span, from s rounded down to 4
-      const uint32_t need = e_lo + (verify ? 4u : 0u);
-      const uint32_t a_lo = ((need + 3u) & ~3u) - 16u;  // 16 <= n + 7: a_lo may precede s
+      // span's last byte -- or, when they would start in the page below a
+      // short span, from s rounded down to 4
+      const uint32_t e_lo = s_lo + n;
+      const uint32_t a_lo = ((e_lo + 3u) & ~3u) - 16u;  // 16 <= n + 3: a_lo may precede s
       const uint32_t before = s_lo - a_lo;              // bytes in front of s (mod 2^32)
       const uint32_t a_fix = (before <= 16u && before > pg) ? (s_lo & ~3u) : a_lo;
       axd = (a_fix - s_lo) + hp;  // from c0 = s - hp
-      const uint32_t te = (e_lo - k - a_fix) & 15u;
-      const uint32_t tv = (e_lo - a_fix) & 15u;
-      geo |= (te << 8) | (tv << 12);
+      geo |= ((e_lo - k - a_fix) & 15u) << 8;
     } else {
       axd = 0;
     }
   }
-  WIPDB_LK_HD inline SegE next(bool verify) {
+  WIPDB_LK_HD inline SegE next() {
     SegE g;
     const bool last = j + 1u == nseg;
     const uint32_t hp = geo & 15u, ws = (geo >> 4) & 3u, k = (geo >> 6) & 3u;
     const uint32_t nc0 = geo >> 18;
     uint32_t fl = kEValid | (last ? kELast : 0u);
-    // (a piece span's tail word / trailer come with its piece, PieceChunkOffset)
-    if (last && (verify || k != 0u) && !(geo & (1u << 16))) fl |= kEAux;
+    // (a piece span's tail word comes with its piece, PieceChunkOffset)
+    if (last && k != 0u && !(geo & (1u << 16))) fl |= kEAux;
     g.c.init = init;
     g.c.id = id;
     g.c.c0 = c0;
-    g.c.g2 = (geo >> 12) & 15u;
+    g.c.g2 = (geo >> 12) & 3u;
     g.ax = c0 + static_cast<uint64_t>(static_cast<int64_t>(static_cast<int32_t>(axd)));
     g.src0 = 0;
     uint32_t front = 0, h = 0, w = 0;
@@ -212,24 +221,40 @@ WIPDB_LK_HD inline uint32_t SegChunkOffset(const SegE& g, uint32_t t) {
 // The DMA source of window chunk t (0..15) of a front piece with ring word
 // pw (chunks | hp << 8 | ws << 12 | k << 14), from sbase + its c0.
 // Window chunk 0 (always in front of a piece of <= kPieceMax chunks) instead
-// reads the span's aux chunk: the 16 bytes ending at the 4-byte word holding
-// its last byte (verify: its trailer's last byte), i.e. at offset
-// 16 (C - 1) + 4 verify + 4 [k > 0] from chunk 0, C = 256 + piece chunks;
-// the tail word is at byte PieceTailAt, the trailer at PieceTrailerAt.
-WIPDB_LK_HD inline uint32_t PieceAuxOffset(uint32_t pw, bool verify) {
-  const uint32_t k = (pw >> 14) & 3u;
-  return 16u * (kSegChunks + (pw & 63u) - 1u) + (verify ? 4u : 0u) + (k != 0u ? 4u : 0u);
-}
-WIPDB_LK_HD inline uint32_t PieceTailAt(uint32_t pw, bool verify) {
-  return 16u - (verify ? 4u : 0u) - (((pw >> 14) & 3u) != 0u ? 4u : 0u);
-}
-WIPDB_LK_HD inline uint32_t PieceTrailerAt(uint32_t pw) { return PieceTailAt(pw, true) + ((pw >> 14) & 3u); }
-WIPDB_LK_HD inline uint32_t PieceChunkOffset(uint32_t pw, uint32_t t, bool verify) {
-  if (t == 0u) return PieceAuxOffset(pw, verify);
+// reads the span's aux chunk when it has a tail: the 16 bytes ending at the
+// 4-byte word holding its last byte, i.e. at offset 16 (C - 1) + 4 from
+// chunk 0, C = 256 + piece chunks; the tail word is its last word.  (A
+// verify span has no tail: its grid holds the trailer, WalkE::start.)
+WIPDB_LK_HD inline uint32_t PieceChunkOffset(uint32_t pw, uint32_t t) {
+  if (t == 0u && (pw & (3u << 14)) != 0u) return 16u * (kSegChunks + (pw & 63u)) - 12u;
   const int32_t front = static_cast<int32_t>(kPieceChunks - (pw & 63u));
   const int32_t s0 = static_cast<int32_t>(4u * ((pw >> 12) & 3u));
   const int32_t b = 16 * (static_cast<int32_t>(t) - front);
   return static_cast<uint32_t>(b > s0 ? b : s0);
+}
+
+// ---- verify: the CRC residue ----
+// A verify span's grid ends jv <= 3 bytes past its stored trailer, so the
+// last 8 bytes of its last (or main) segment -- words 14 and 15 of lane 63's
+// last chunk -- hold the trailer at byte 4 - jv.  fix_trailer unmasks it in
+// place and zeroes the jv bytes after it; the register after the block ||
+// Unmask(trailer) || jv zero bytes is then the constant verify_residue(jv)
+// exactly when the trailer matches (feeding a word w: r -> zero-feed(r ^ w,
+// 4), and r ^ crc = ~0 for the register r = ~crc of the block; zero-feeds
+// are bijections), so no lane needs the trailer as a value.
+WIPDB_LK_HD constexpr uint32_t verify_residue(uint32_t jv) {
+  uint32_t r = ~0u;
+  for (uint32_t i = 0; i < 8u * (4u + jv); ++i) r = (r >> 1) ^ (0x82f63b78u & (0u - (r & 1u)));
+  return r;
+}
+WIPDB_LK_HD inline void fix_trailer(uint32_t& lo, uint32_t& hi, uint32_t jv) {
+  const uint64_t x = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+  const uint32_t sh = 8u * (4u - jv);  // 8 .. 32
+  const uint32_t r = static_cast<uint32_t>(x >> sh) - 0xa282ead8u;
+  const uint32_t c = (r >> 17) | (r << 15);
+  const uint64_t y = (x & ((uint64_t(1) << sh) - 1u)) | (static_cast<uint64_t>(c) << sh);
+  lo = static_cast<uint32_t>(y);
+  hi = static_cast<uint32_t>(y >> 32);
 }
 
 // Chunk 0 of a span into its span form: read ws words late (shift right by
