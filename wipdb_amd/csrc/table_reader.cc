@@ -8,7 +8,6 @@
 #include <stdint.h>
 
 #include <algorithm>
-#include <queue>
 #include <string>
 #include <vector>
 
@@ -47,7 +46,8 @@ uint32_t StoredCrc(const char* image, const Handle& h) {
 // Entries of a block (kv/src/table/block.cc): the values, in order.  Fails
 // like Block's constructor / iterator ("bad block contents", "bad entry in
 // block").
-Status BlockValues(std::string_view b, std::vector<std::pair<std::string, std::string_view>>* kv) {
+template <class Sink>
+Status ForEachEntry(std::string_view b, std::string* key, Sink&& sink) {
   if (b.size() < 4) return Status::Corruption("bad block contents");
   const uint32_t nrest = sst::DecodeFixed32(b.data() + b.size() - 4);
   if (nrest > (b.size() - 4) / 4) return Status::Corruption("bad block contents");
@@ -56,20 +56,24 @@ Status BlockValues(std::string_view b, std::vector<std::pair<std::string, std::s
   // SeekToFirst: the first entry is at restart point 0 (block.cc SeekToRestartPoint)
   const char* p = b.data() + sst::DecodeFixed32(b.data() + limit_off);
   const char* limit = b.data() + limit_off;
-  std::string key;
+  key->clear();
   while (p < limit) {
     uint32_t shared, non_shared, vlen;
     p = sst::GetVarint32(p, limit, &shared);
     if (p) p = sst::GetVarint32(p, limit, &non_shared);
     if (p) p = sst::GetVarint32(p, limit, &vlen);
-    if (!p || static_cast<size_t>(limit - p) < size_t(non_shared) + vlen || shared > key.size())
+    if (!p || static_cast<size_t>(limit - p) < size_t(non_shared) + vlen || shared > key->size())
       return Status::Corruption("bad entry in block");
-    key.resize(shared);
-    key.append(p, non_shared);
-    kv->emplace_back(key, std::string_view(p + non_shared, vlen));
+    key->resize(shared);
+    key->append(p, non_shared);
+    sink(*key, std::string_view(p + non_shared, vlen));
     p += non_shared + vlen;
   }
   return Status::OK();
+}
+Status BlockValues(std::string_view b, std::vector<std::pair<std::string, std::string_view>>* kv) {
+  std::string key;
+  return ForEachEntry(b, &key, [kv](const std::string& k, std::string_view v) { kv->emplace_back(k, v); });
 }
 
 struct TableJob {
@@ -301,9 +305,19 @@ struct CompactionInput::Rep {
     std::vector<uint8_t> chk;    // per block: kUnchecked / kGood / kBadCrc / kShort
     size_t next_check = 0;       // first block not yet sent to a CRC batch
     size_t bi = 0;               // current block
-    std::vector<std::pair<std::string, std::string_view>> ents;
+    // the current block's entries: keys back to back in `arena`, values
+    // viewing the image
+    struct Ent {
+      uint32_t ko, kl;
+      const char* v;
+      size_t vl;
+    };
+    std::string arena, scratch;
+    std::vector<Ent> ents;
     size_t ei = 0;
     bool valid = false;
+    std::string_view key() const { return {arena.data() + ents[ei].ko, ents[ei].kl}; }
+    std::string_view value() const { return {ents[ei].v, ents[ei].vl}; }
     void Save(const Status& s) {
       if (saved.ok() && !s.ok()) saved = s;
     }
@@ -318,16 +332,38 @@ struct CompactionInput::Rep {
   std::vector<In> in;
   uint64_t batches = 0, checked = 0;
   Status fatal;  // a device error of a CRC batch (kBatchGpu)
-  // merge: the input holding the smallest key (ties: the lower input)
-  struct Later {
-    const Rep* r;
-    bool operator()(size_t a, size_t b) const {
-      const int c = r->cmp->Compare(r->in[a].ents[r->in[a].ei].first, r->in[b].ents[r->in[b].ei].first);
-      return c > 0 || (c == 0 && a > b);
-    }
-  };
-  std::priority_queue<size_t, std::vector<size_t>, Later> heap{Later{this}};
+  // merge: a binary min-heap of the valid inputs by current key (ties: the
+  // lower input first, merger.cc's order); the top is the current entry and
+  // Next() re-sifts it in place
+  std::vector<size_t> heap;
   size_t cur = SIZE_MAX;
+  bool Before(size_t a, size_t b) const {
+    const int c = cmp->Compare(in[a].key(), in[b].key());
+    return c < 0 || (c == 0 && a < b);
+  }
+  void SiftDown(size_t pos) {
+    const size_t n = heap.size();
+    const size_t item = heap[pos];
+    for (;;) {
+      size_t c = 2 * pos + 1;
+      if (c >= n) break;
+      if (c + 1 < n && Before(heap[c + 1], heap[c])) ++c;
+      if (!Before(heap[c], item)) break;
+      heap[pos] = heap[c];
+      pos = c;
+    }
+    heap[pos] = item;
+  }
+  void SiftUp(size_t pos) {
+    const size_t item = heap[pos];
+    while (pos > 0) {
+      const size_t p = (pos - 1) / 2;
+      if (!Before(item, heap[p])) break;
+      heap[pos] = heap[p];
+      pos = p;
+    }
+    heap[pos] = item;
+  }
 
   void Open() {
     // Table::Open(paranoid_checks) of every input: one batch of index blocks
@@ -430,6 +466,7 @@ struct CompactionInput::Rep {
     for (; b < x.blocks.size(); ++b) {
       x.bi = b;
       x.ents.clear();
+      x.arena.clear();
       x.ei = 0;
       if (!x.bad_handle[b].ok()) {
         x.Save(x.bad_handle[b]);
@@ -453,7 +490,13 @@ struct CompactionInput::Rep {
         x.Save(ts);
         continue;
       }
-      x.Save(BlockEntries(std::string_view(x.img + h.offset, h.size), &x.ents));
+      x.Save(ForEachEntry(std::string_view(x.img + h.offset, h.size), &x.scratch,
+                          [&x](const std::string& k, std::string_view v) {
+                            x.ents.push_back(In::Ent{static_cast<uint32_t>(x.arena.size()),
+                                                     static_cast<uint32_t>(k.size()), v.data(),
+                                                     v.size()});
+                            x.arena.append(k);
+                          }));
       if (!x.ents.empty()) {
         x.valid = true;
         return;
@@ -471,7 +514,7 @@ struct CompactionInput::Rep {
   void Pick() {
     cur = SIZE_MAX;
     if (!fatal.ok() || heap.empty()) return;
-    cur = heap.top();
+    cur = heap[0];
   }
 };
 
@@ -493,7 +536,7 @@ CompactionInput::~CompactionInput() { delete rep_; }
 
 void CompactionInput::SeekToFirst() {
   Rep* r = rep_;
-  r->heap = decltype(r->heap)(Rep::Later{r});
+  r->heap.clear();
   for (auto& x : r->in) {
     x.saved = Status::OK();
     x.valid = false;
@@ -503,7 +546,10 @@ void CompactionInput::SeekToFirst() {
     Rep::In& x = r->in[i];
     if (!x.open.ok()) continue;
     r->Load(x, 0);
-    if (x.valid) r->heap.push(i);
+    if (x.valid) {
+      r->heap.push_back(i);
+      r->SiftUp(r->heap.size() - 1);
+    }
   }
   r->Pick();
 }
@@ -512,21 +558,22 @@ bool CompactionInput::Valid() const { return rep_->cur != SIZE_MAX; }
 
 void CompactionInput::Next() {
   Rep* r = rep_;
-  const size_t i = r->cur;
-  r->heap.pop();
+  const size_t i = r->cur;  // == heap[0]
   r->Step(i);
-  if (r->in[i].valid) r->heap.push(i);
+  if (!r->in[i].valid) {
+    r->heap[0] = r->heap.back();
+    r->heap.pop_back();
+  }
+  if (!r->heap.empty()) r->SiftDown(0);
   r->Pick();
 }
 
 std::string_view CompactionInput::key() const {
-  const Rep::In& x = rep_->in[rep_->cur];
-  return x.ents[x.ei].first;
+  return rep_->in[rep_->cur].key();
 }
 
 std::string_view CompactionInput::value() const {
-  const Rep::In& x = rep_->in[rep_->cur];
-  return x.ents[x.ei].second;
+  return rep_->in[rep_->cur].value();
 }
 
 Status CompactionInput::status() const {
