@@ -47,6 +47,10 @@ struct Drop {
 // (recycle_log_files, log_number) that starts at a block boundary would.
 Status WriteLog(const std::vector<std::string_view>& records, bool recycle, uint64_t log_number,
                 table::CrcMode mode, int device, std::string* out);
+// WriteLog straight into a caller's buffer of cap bytes: *size = the image
+// size; InvalidArgument (nothing written) when it exceeds cap.
+Status WriteLogTo(const std::vector<std::string_view>& records, bool recycle, uint64_t log_number,
+                  table::CrcMode mode, int device, char* out, size_t cap, size_t* size);
 
 // Recovery read of one log image (checksum = true, initial offset 0).
 Status ReadLog(const char* image, size_t n, table::CrcMode mode, int device,
@@ -56,6 +60,15 @@ Status ReadLog(const char* image, size_t n, table::CrcMode mode, int device,
 Status ReadLogs(const char* const* images, const size_t* sizes, size_t nlogs,
                 table::CrcMode mode, int device, std::vector<std::vector<Record>>* records,
                 std::vector<std::vector<Drop>>* drops);
+
+// ReadLogs handing each record to fn(ctx, log, LastRecordOffset, data, size)
+// in order instead of copying it into a Record: a record of one fragment is
+// a view of the image, a fragmented one a view of scratch valid during the
+// call.
+typedef void (*RecordFn)(void* ctx, size_t log, uint64_t offset, const char* data, size_t n);
+Status ReadLogsEach(const char* const* images, const size_t* sizes, size_t nlogs,
+                    table::CrcMode mode, int device, RecordFn fn, void* ctx,
+                    std::vector<std::vector<Drop>>* drops);
 
 }  // namespace log
 }  // namespace wipdb

@@ -178,13 +178,12 @@ int wsst_log_write(const char* records, const uint32_t* lens, size_t n, int recy
     recs[i] = std::string_view(records + o, lens[i]);
     o += lens[i];
   }
-  std::string img;
-  const Status s = wipdb::log::WriteLog(recs, recycle != 0, log_number, mode, device, &img);
-  if (!s.ok()) return Code(s);
-  *out_size = img.size();
-  if (img.size() > cap) return WSST_ERR_TOO_SMALL;
-  memcpy(out, img.data(), img.size());
-  return WSST_OK;
+  size_t size = 0;
+  const Status s =
+      wipdb::log::WriteLogTo(recs, recycle != 0, log_number, mode, device, out, cap, &size);
+  *out_size = size;
+  if (size > cap) return WSST_ERR_TOO_SMALL;
+  return s.ok() ? WSST_OK : Code(s);
 }
 
 int wsst_log_read(const char* const* images, const size_t* sizes, size_t nlogs, int crc_mode,
@@ -195,27 +194,38 @@ int wsst_log_read(const char* const* images, const size_t* sizes, size_t nlogs, 
   CrcMode mode;
   if (!ModeOf(crc_mode, &mode) || (nlogs && (!images || !sizes || !nrecs || !ndrops)))
     return WSST_ERR_INVALID;
-  std::vector<std::vector<wipdb::log::Record>> recs;
+  struct Out {
+    char* rec_out;
+    size_t rec_cap, max_recs, r = 0, used = 0;
+    uint32_t* rec_lens;
+    uint64_t* rec_offsets;
+    uint64_t* nrecs;
+    bool full = false;
+  } o{rec_out, rec_cap, max_recs, 0, 0, rec_lens, rec_offsets, nrecs};
+  for (size_t i = 0; i < nlogs; ++i) nrecs[i] = 0;
   std::vector<std::vector<wipdb::log::Drop>> drops;
-  const Status s = wipdb::log::ReadLogs(images, sizes, nlogs, mode, device, &recs, &drops);
+  const Status s = wipdb::log::ReadLogsEach(
+      images, sizes, nlogs, mode, device,
+      [](void* c, size_t log, uint64_t off, const char* d, size_t n) {
+        Out& o = *static_cast<Out*>(c);
+        ++o.nrecs[log];
+        if (o.full || o.r >= o.max_recs || o.used + n > o.rec_cap || !o.rec_out || !o.rec_lens ||
+            !o.rec_offsets) {
+          o.full = true;
+          return;
+        }
+        memcpy(o.rec_out + o.used, d, n);
+        o.rec_lens[o.r] = static_cast<uint32_t>(n);
+        o.rec_offsets[o.r] = off;
+        o.used += n;
+        ++o.r;
+      },
+      &o, &drops);
   if (!s.ok()) return Code(s);
-  size_t r = 0, d = 0, used = 0;
-  int rc = WSST_OK;
+  int rc = o.full ? WSST_ERR_TOO_SMALL : WSST_OK;
+  size_t d = 0;
   for (size_t i = 0; i < nlogs; ++i) {
-    nrecs[i] = recs[i].size();
     ndrops[i] = drops[i].size();
-    for (const auto& x : recs[i]) {
-      if (r >= max_recs || used + x.data.size() > rec_cap || !rec_out || !rec_lens ||
-          !rec_offsets) {
-        rc = WSST_ERR_TOO_SMALL;
-        break;
-      }
-      memcpy(rec_out + used, x.data.data(), x.data.size());
-      rec_lens[r] = static_cast<uint32_t>(x.data.size());
-      rec_offsets[r] = x.offset;
-      used += x.data.size();
-      ++r;
-    }
     for (const auto& x : drops[i]) {
       if (d >= max_drops || !drop_bytes || !drop_reasons) {
         rc = WSST_ERR_TOO_SMALL;
