@@ -47,7 +47,7 @@ __device__ __forceinline__ void dma4(uint64_t base, uint32_t slot, uint32_t o0, 
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(o0), "v"(o1), "v"(o2), "v"(o3), "s"(slot), "s"(base)
-      : "memory");
+      : "memory", "scc");
 }
 
 // Wave w of workgroup g takes blocks g*16 + w, + 16 * grid, ...; one block

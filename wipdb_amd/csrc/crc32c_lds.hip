@@ -266,7 +266,7 @@ __device__ __forceinline__ void dma4(uint64_t base, uint32_t slot, uint32_t o0, 
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(o0), "v"(o1), "v"(o2), "v"(o3), "s"(slot), "s"(base)
-      : "memory");
+      : "memory", "scc");
 }
 
 __device__ __forceinline__ void dma1(uint64_t base, uint32_t dst, uint32_t off) {
@@ -295,7 +295,7 @@ __device__ __forceinline__ void dma2(uint64_t base, uint32_t slot, uint32_t o0, 
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(o0), "v"(o1), "s"(slot), "s"(base)
-      : "memory");
+      : "memory", "scc");
 }
 
 __device__ __forceinline__ void dma1nt(uint64_t base, uint32_t dst, uint32_t off) {
