@@ -704,13 +704,24 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       ring.head = (ring.head + n) & 63u;
       ring.count -= n;
     } else if (more) {
+      bool fast = false;
       if (!wk.valid) {
-        wk.start(sbase, pf.d, kVerify);
         took_pf = true;
+        uint64_t wb;
+        fast = FastSeg(sbase, pf.d, kVerify, nxt, wb);
+        if (fast) {
+          // a simple span or a table block's main segment: one full window
+          const uint32_t o = 16u * pp.cm;
+          dma4(sbase + wb, pp.slot, o, o + 1024u, o + 2048u, o + 3072u);
+        } else {
+          wk.start(sbase, pf.d, kVerify);
+        }
       }
-      const SegE g = wk.next();
-      issue(g);
-      nxt = g.c;
+      if (!fast) {
+        const SegE g = wk.next();
+        issue(g);
+        nxt = g.c;
+      }
     }
 
     bool did_store = false;
@@ -756,6 +767,24 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
           const uint32_t v = tail_step(lk, sft ^ T, tw, k);
           out32[sid] = msk ? mask_crc(~v) : ~v;
         }
+      }
+      did_store = true;
+    } else if (kVerify && (cur.flags() & kESimple)) {
+      // ---- a simple verify span (the spans kernel measured faster through
+      // the general segment code below): ~init enters at word 0, the stored
+      // trailer is unmasked in place, a good block leaves the residue ----
+      W[0] ^= l == 0u ? ~cur.init : 0u;
+      uint32_t lo = W[14], hi = W[15];
+      fix_trailer(lo, hi, cur.jv());
+      W[14] = l == 63u ? lo : W[14];
+      W[15] = l == 63u ? hi : W[15];
+      const uint32_t R = fold<1>(lk, l, scan(lk, W))[0];
+      if (l == 0u) {
+        constexpr uint32_t kRes0 = verify_residue(0), kRes1 = verify_residue(1),
+                           kRes2 = verify_residue(2), kRes3 = verify_residue(3);
+        const uint32_t jv = cur.jv();
+        const uint32_t res = jv == 0u ? kRes0 : (jv == 1u ? kRes1 : (jv == 2u ? kRes2 : kRes3));
+        out8[cur.id] = R == res ? 1u : 0u;
       }
       did_store = true;
     } else {

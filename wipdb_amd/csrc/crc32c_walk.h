@@ -61,7 +61,7 @@ WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {
 //   register = piece register * x^(8 * 4096) ^ main register, then the tail.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kEValid = 1u, kEFirst = 2u, kELast = 4u, kEMain = 8u, kEBatch = 16u,
-                   kENoBody = 32u, kEAux = 64u;
+                   kENoBody = 32u, kEAux = 64u, kESimple = 128u;
 constexpr uint32_t kPieceChunks = 16;  // a piece window: 4 lanes x 4 chunks
 constexpr uint32_t kPieceMax = 15;     // piece chunks: window chunk 0 stays free for the aux chunk
 constexpr uint32_t kBatch = 16;        // pieces per batch iteration
@@ -97,6 +97,53 @@ struct SegE {
   uint64_t ax;    // last: offset of the 16 bytes holding the tail word
   uint32_t src0;  // DMA offset (from wb) of the span's chunk 0, also read by the in-front lanes
 };
+
+// The two common span shapes without the walk (scalar work per span is the
+// kernels' scarce resource):
+//   * a SIMPLE span, one whole 256-chunk window: a 4-byte aligned start and a
+//     body (+ the verify trailer) of exactly 4096 bytes -- hp = ws = k = 0,
+//     no piece, no aux chunk (the aligned 4 KiB block; ReadBlock on a
+//     4091-byte block).  g1 = kEValid | kEFirst | kELast | kESimple;
+//   * a TABLE BLOCK, 257..271 chunks: one full main segment + a front piece.
+// Fills the segment (and its window base wb) exactly as WalkE::start + next
+// would -- tests/cpp/test_walk.cc checks it -- except for the kESimple flag
+// and a main segment's te (unused there: its tail rides with the piece).
+// Returns false for any other shape: the walk takes it.
+WIPDB_LK_HD inline bool FastSeg(uint64_t sbase, const SpanD& d, bool verify, SegC& c, uint64_t& wb) {
+  const uint32_t n = d.n;
+  const uint32_t s_lo = static_cast<uint32_t>(sbase) + static_cast<uint32_t>(d.a);
+  uint32_t k, nb, jv;
+  if (verify) {
+    jv = (0u - (s_lo + n + 4u)) & 3u;
+    k = 0;
+    nb = n + 4u + jv;
+  } else {
+    jv = 0;
+    const uint32_t e3 = (s_lo + n) & 3u;
+    k = e3 < n ? e3 : n;
+    nb = n - k;
+  }
+  const uint32_t C = (nb + 15u) >> 4;
+  const uint32_t hp = (C << 4) - nb;
+  c.init = d.init;
+  c.id = static_cast<uint32_t>(d.id);
+  if (C == kSegChunks && (hp | k) == 0u) {
+    c.g1 = kEValid | kEFirst | kELast | kESimple;
+    c.g2 = jv;
+    c.c0 = d.a;
+    wb = d.a;
+    return true;
+  }
+  if (C - (kSegChunks + 1u) >= kPieceMax) return false;  // not 257..271
+  const uint32_t pg = s_lo & 4095u;
+  const uint32_t ws = pg < hp ? (hp - (pg & 3u)) >> 2 : 0u;
+  const uint32_t nc0 = C - kSegChunks;
+  c.c0 = d.a - hp;
+  wb = c.c0 + 16u * nc0;
+  c.g1 = kEValid | kELast | kEMain | (k << 23);
+  c.g2 = jv | (nc0 << 4) | (hp << 9) | (ws << 13);
+  return true;
+}
 
 struct WalkE {
   uint64_t c0;
