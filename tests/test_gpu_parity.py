@@ -229,6 +229,42 @@ def test_near_4k_lengths_every_pad(engine, oracle):
     np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
 
 
+def test_fast_path_shapes_crc_and_verify(engine, oracle):
+    """The kernels' walk-free shapes (FastSeg: a 4-byte aligned 4 KiB body;
+    a table block of 257..271 chunks = main segment + front piece) and their
+    neighbours, at starts around a page boundary (the piece's head read late,
+    ws != 0) and at every 4-byte phase: CRCs with inits, then ReadBlock's
+    verify (n + 1 bytes, masked trailer) good and with one flipped byte."""
+    rng = np.random.default_rng(4089)
+    lens = np.arange(4084, 4341, dtype=np.uint32)           # simple, pieces 1..15, tails 0..3
+    phases = [0, 1, 2, 3, 4, 8, 13, 16, 4096 - 1, 4096 - 3, 4096 - 4, 4096 - 12, 4096 - 15]
+    slot = 16384
+    n_sp = lens.size * len(phases)
+    buf = rng.integers(0, 256, n_sp * slot + 8192, dtype=np.uint8)
+    ln = np.repeat(lens, len(phases))
+    # one span per 16 KiB slot, starting at a phase around the slot's second page
+    offs = np.array([k * slot + 4096 + phases[k % len(phases)] for k in range(ln.size)], np.uint64)
+    inits = rng.integers(0, 2**32, size=ln.size, dtype=np.uint64).astype(np.uint32)
+    inits[::2] = 0
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, ln, inits),
+                                  oracle.batch(buf, offs, ln, inits))
+    # verify: handle size n (contents + type = n + 1 bytes), trailer after
+    vl = ln - 1
+    for o, n in zip(offs, vl):
+        crc = oracle.extend(0, buf, int(o), int(n) + 1)
+        m = int(oracle.lib.oracle_mask(crc))
+        buf[int(o) + n + 1:int(o) + n + 5] = np.frombuffer(m.to_bytes(4, "little"), np.uint8)
+    bad = rng.choice(ln.size, 64, replace=False)
+    for i, b in enumerate(bad):
+        buf[int(offs[b]) + int(rng.integers(0, int(vl[b]) + 5))] ^= 1 << (i % 8)
+    import torch
+    st = engine.verify_device(_t(buf), _t(offs), _t(vl))
+    torch.cuda.synchronize()
+    expect = np.ones(ln.size, np.uint8)
+    expect[bad] = 0
+    np.testing.assert_array_equal(st.cpu().numpy(), expect)
+
+
 @pytest.mark.parametrize("count", [1, 2, 31, 32, 33, 255, 8191, 8192, 8193, 24581, 40000])
 def test_batch_counts_work_sharing(engine, oracle, count):
     """Batch sizes around the grid's round (8192 groups on 256 CUs) and the
