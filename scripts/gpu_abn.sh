@@ -14,7 +14,7 @@ for r in $(seq 1 "$ROUNDS"); do
   for v in "$@"; do
     if [ "$v" = tree ]; then unset WIPDB_HCRC_LIB; else export WIPDB_HCRC_LIB=$PWD/$v; fi
     timeout -k 10 120 python bench.py --no-cpu-baseline --steps 50 > gpurun_out/ab_bench.log 2>&1 || exit $?
-    b=$(grep -o '"kernel_avg_ms": [0-9.]*' gpurun_out/ab_bench.log)
+    b=$(grep -o '"kernel_avg_ms": [0-9.]*\|"mismatches": [0-9]*' gpurun_out/ab_bench.log | tr '\n' ' ')
     e=""
     if [ -n "$WHAT" ] && [ "$WHAT" != none ]; then
       timeout -k 10 200 python scripts/bench_extra.py --what "$WHAT" > gpurun_out/ab_extra.log 2>&1 || exit $?
