@@ -70,6 +70,7 @@ extern "C" {
 #define HCRC_ERR_HIP (-4)       /* other HIP runtime error               */
 #define HCRC_ERR_LAUNCH (-5)    /* kernel launch failed                  */
 #define HCRC_ERR_MISMATCH (-6)  /* hcrc_verify*: at least one bad block  */
+#define HCRC_ERR_BOUNDS (-7)    /* hcrc_check_spans: a span leaves base   */
 
 /* flags */
 #define HCRC_HOST_PTRS 0x0    /* all array/data pointers are host memory    */
@@ -132,6 +133,24 @@ int hcrc_verify_async(hcrc_ctx* ctx, const void* d_base,
 int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base,
                          const uint64_t* d_offsets, const uint32_t* d_lengths,
                          uint8_t* d_status, size_t count, int flags, void* stream);
+
+/* Bounds check of a device descriptor batch before it is handed to the
+ * kernels, which trust it (a span outside the caller's buffer is a GPU page
+ * fault).  Span i is out of bounds when offsets[i] + lengths[i] + extra >
+ * base_bytes, computed without overflow; extra = 0 for a CRC batch, 5 for a
+ * verify batch (type byte + stored crc).  The async form writes
+ * d_result[0] = the number of such spans and d_result[1] = the lowest such
+ * index (UINT64_MAX if none) on `stream`; the synchronous form returns
+ * HCRC_OK or HCRC_ERR_BOUNDS (with *first_bad, nullable).  The reference's
+ * equivalent is the size check ReadBlock makes on the pread result
+ * (kv/src/table/format.cc:84-87). */
+int hcrc_check_spans_async(hcrc_ctx* ctx, uint64_t base_bytes,
+                           const uint64_t* d_offsets, const uint32_t* d_lengths,
+                           uint32_t extra, size_t count, uint64_t* d_result,
+                           void* stream);
+int hcrc_check_spans(hcrc_ctx* ctx, uint64_t base_bytes,
+                     const uint64_t* d_offsets, const uint32_t* d_lengths,
+                     uint32_t extra, size_t count, uint64_t* first_bad);
 
 /* Wait for all work on `stream` (NULL = the HIP default stream). */
 int hcrc_sync(hcrc_ctx* ctx, void* stream);

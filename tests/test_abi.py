@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
 def test_abi_version_and_strerror():
     lib = _lib.load()
     assert lib.hcrc_abi_version() == 1
-    for code in (0, -1, -2, -3, -4, -5, -6, -99):
+    for code in (0, -1, -2, -3, -4, -5, -6, -7, -99):
         assert lib.hcrc_strerror(code)
 
 
@@ -36,6 +36,8 @@ def test_invalid_arguments_are_rejected_without_device():
     assert lib.hcrc_batch(None, None, None, None, None, None, 0, 0) == _lib.HCRC_ERR_INVALID
     assert lib.hcrc_batch_async(None, None, None, None, None, None, 0, 1, None) == _lib.HCRC_ERR_INVALID
     assert lib.hcrc_sync(None, None) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_check_spans(None, 0, None, None, 0, 0, None) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_check_spans_async(None, 0, None, None, 0, 0, None, None) == _lib.HCRC_ERR_INVALID
     devs = (ctypes.c_int * 1)(0)
     assert lib.hcrc_batch_multi(devs, 0, None, None, None, None, None, 0, 0) == _lib.HCRC_ERR_INVALID
     assert lib.hcrc_cpu_batch(None, None, None, None, None, 1, 0, 1) == _lib.HCRC_ERR_INVALID

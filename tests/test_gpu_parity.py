@@ -265,6 +265,56 @@ def test_fast_path_shapes_crc_and_verify(engine, oracle):
     np.testing.assert_array_equal(st.cpu().numpy(), expect)
 
 
+def test_check_spans_bounds(engine):
+    """hcrc_check_spans: the count and lowest index of spans that leave the
+    base buffer, overflow-safe, for CRC (extra 0) and verify (extra 5)
+    batches; the Python entry points refuse such a batch before launching."""
+    import ctypes
+    import torch
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    size = 1 << 20
+    base = torch.zeros(size, dtype=torch.uint8, device="cuda:0")
+    rng = np.random.default_rng(3)
+    n = 100_000
+    lens = rng.integers(0, 9000, n).astype(np.uint32)
+    offs = (rng.integers(0, size - 9000 - 5, n)).astype(np.uint64)
+    d_off, d_len = _t(offs), _t(lens)
+    first = ctypes.c_uint64(7)
+    assert lib.hcrc_check_spans(engine._ctx, size, d_off.data_ptr(), d_len.data_ptr(), 5, n,
+                                ctypes.byref(first)) == 0
+    bad = np.sort(rng.choice(n, 37, replace=False))
+    offs2, lens2 = offs.copy(), lens.copy()
+    for i, b in enumerate(bad):
+        if i % 3 == 0:
+            offs2[b] = size - lens2[b] + 1          # one byte past the end
+        elif i % 3 == 1:
+            offs2[b] = (1 << 64) - 16               # offset + length wraps around
+        else:
+            offs2[b] = size + 4096                  # starts past the end
+    d_off2, d_len2 = _t(offs2), _t(lens2)
+    rc = lib.hcrc_check_spans(engine._ctx, size, d_off2.data_ptr(), d_len2.data_ptr(), 0, n,
+                              ctypes.byref(first))
+    assert rc == _lib.HCRC_ERR_BOUNDS and first.value == bad[0]
+    res = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    assert lib.hcrc_check_spans_async(engine._ctx, size, d_off2.data_ptr(), d_len2.data_ptr(), 0, n,
+                                      res.data_ptr(), engine.stream) == 0
+    engine.sync(engine.stream)
+    r = res.cpu().numpy().view(np.uint64)
+    assert int(r[0]) == bad.size and int(r[1]) == bad[0]
+    # an exact fit passes; one more byte (or the verify trailer) fails
+    o1, l1 = _t(np.array([size - 100], np.uint64)), _t(np.array([100], np.uint32))
+    assert lib.hcrc_check_spans(engine._ctx, size, o1.data_ptr(), l1.data_ptr(), 0, 1, None) == 0
+    assert lib.hcrc_check_spans(engine._ctx, size, o1.data_ptr(), l1.data_ptr(), 5, 1,
+                                None) == _lib.HCRC_ERR_BOUNDS
+    with pytest.raises(IndexError):
+        engine.batch_device(base, d_off2, d_len2, check_bounds=True)
+    with pytest.raises(IndexError):
+        engine.verify_device(base, o1, l1, check_bounds=True)
+    engine.batch_device(base, d_off, d_len, check_bounds=True)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("count", [1, 2, 31, 32, 33, 255, 8191, 8192, 8193, 24581, 40000])
 def test_batch_counts_work_sharing(engine, oracle, count):
     """Batch sizes around the grid's round (8192 groups on 256 CUs) and the

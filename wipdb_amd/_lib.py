@@ -24,6 +24,7 @@ HCRC_ERR_NO_MEMORY = -3
 HCRC_ERR_HIP = -4
 HCRC_ERR_LAUNCH = -5
 HCRC_ERR_MISMATCH = -6
+HCRC_ERR_BOUNDS = -7
 
 HCRC_HOST_PTRS = 0x0
 HCRC_DEVICE_PTRS = 0x1
@@ -62,6 +63,10 @@ _PROTOS = {
     "hcrc_host_register": (_c.c_int, [_vp, _sz]),
     "hcrc_host_unregister": (_c.c_int, [_vp]),
     "hcrc_readstream_async": (_c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint32, _vp, _sz, _vp]),
+    "hcrc_check_spans_async": (
+        _c.c_int, [_vp, _c.c_uint64, _vp, _vp, _c.c_uint32, _sz, _vp, _vp]),
+    "hcrc_check_spans": (
+        _c.c_int, [_vp, _c.c_uint64, _vp, _vp, _c.c_uint32, _sz, _c.POINTER(_c.c_uint64)]),
     "hcrc_fill_splitmix64_async": (
         _c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint64, _c.c_uint64, _vp]),
     "hcrc_cpu_extend": (_c.c_uint32, [_c.c_uint32, _vp, _sz]),

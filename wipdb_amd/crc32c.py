@@ -176,7 +176,8 @@ class Engine:
         import torch
         return torch.device("cuda", self.device)
 
-    def _check_spans(self, base_t, offsets_t, lengths_t, inits_t, check_bounds: bool) -> int:
+    def _check_spans(self, base_t, offsets_t, lengths_t, inits_t, check_bounds: bool,
+                     extra: int = 0, stream=None) -> int:
         u32, u64, _ = _dtypes()
         dev = self._device()
         _check_tensor(base_t, "base", dev, None)
@@ -185,11 +186,8 @@ class Engine:
         _check_tensor(lengths_t, "lengths", dev, u32, n)
         _check_tensor(inits_t, "inits", dev, u32, n)
         if check_bounds and n:
-            import torch
-            end = offsets_t[:n].to(torch.int64) + lengths_t[:n].to(torch.int64).bitwise_and(0xFFFFFFFF)
             nbytes = base_t.numel() * base_t.element_size()
-            if int(offsets_t[:n].min()) < 0 or int(end.max()) > nbytes:
-                raise ValueError("a span lies outside base")
+            self.check_spans(nbytes, offsets_t, lengths_t, extra, stream)
         return n
 
     def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
@@ -200,9 +198,9 @@ class Engine:
         ``split_small``: HCRC_SPLIT_SMALL (the size classes).  Offsets are
         int64, lengths / inits / out 32-bit, all contiguous on this engine's
         device; ``check_bounds`` also checks every span against base (a
-        device reduction and a sync)."""
+        device kernel and a sync, hcrc_check_spans)."""
         import torch
-        n = self._check_spans(base_t, offsets_t, lengths_t, inits_t, check_bounds)
+        n = self._check_spans(base_t, offsets_t, lengths_t, inits_t, check_bounds, 0, stream)
         if out_t is None:
             out_t = torch.empty(n, dtype=torch.int32, device=base_t.device)
         _check_tensor(out_t, "out", self._device(), _dtypes()[0], n)
@@ -230,14 +228,35 @@ class Engine:
               "hcrc_batch_strided_async")
         return out_t
 
+    def check_spans(self, base_bytes: int, offsets_t, lengths_t, extra: int = 0,
+                    stream=None) -> None:
+        """hcrc_check_spans_async: every span [offsets[i], +lengths[i] + extra)
+        must lie in [0, base_bytes); raises IndexError naming the first that
+        does not.  A device kernel on ``stream`` (default: torch's current,
+        so it sees descriptors written there), then a sync of it."""
+        import torch
+        u32, u64, _ = _dtypes()
+        _check_tensor(offsets_t, "offsets", self._device(), u64)
+        n = int(offsets_t.numel())
+        _check_tensor(lengths_t, "lengths", self._device(), u32, n)
+        res = torch.empty(2, dtype=torch.int64, device=self._device())
+        check(self._lib.hcrc_check_spans_async(self._ctx, int(base_bytes), _ptr(offsets_t),
+                                               _ptr(lengths_t), int(extra), n, _ptr(res),
+                                               self._stream_of(stream)),
+              "hcrc_check_spans_async")
+        self.sync(self._stream_of(stream))
+        bad, first = (int(x) for x in res.cpu().numpy().view(np.uint64))
+        if bad:
+            raise IndexError(f"{bad} span(s) outside base ({base_bytes} bytes), first: {first}")
+
     def verify_device(self, base_t, offsets_t, lengths_t, status_t=None, stream=None,
-                      split_small: bool = False):
+                      split_small: bool = False, check_bounds: bool = False):
         """ReadBlock's check on device blocks: status[i] = 1 iff the stored
         masked crc at byte n+1 matches Value(block, n+1).  ``split_small``:
         HCRC_SPLIT_SMALL (small blocks and table-block remainders on the
         small-span kernel)."""
         import torch
-        n = self._check_spans(base_t, offsets_t, lengths_t, None, False)
+        n = self._check_spans(base_t, offsets_t, lengths_t, None, check_bounds, 5, stream)
         if status_t is None:
             status_t = torch.empty(n, dtype=torch.uint8, device=base_t.device)
         _check_tensor(status_t, "status", self._device(), _dtypes()[2], n)

@@ -1,6 +1,6 @@
 // crc32c_util.hip -- auxiliary device kernels of the library (not the CRC
-// path): the seeded bench/test data generator and the read-stream ceiling
-// the roofline is compared with.
+// path): the seeded bench/test data generator, the read-stream ceiling the
+// roofline is compared with, and the bounds check of device descriptors.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -46,6 +46,41 @@ __global__ __launch_bounds__(256) void fill_splitmix64_kernel(uint64_t* __restri
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     dst[i] = z ^ (z >> 31);
+  }
+}
+
+// Bounds check of a device descriptor batch (hcrc_check_spans_async): span i
+// is bad when offsets[i] + lengths[i] + extra > base_bytes (in 64 bits; an
+// offset past base_bytes is bad whatever the length).  result[0] += the bad
+// spans, result[1] = min(result[1], the lowest bad index); the caller
+// initialises result to {0, ~0}.  One wave-level reduction per 64 spans, one
+// pair of atomics per wave that found any.
+__global__ __launch_bounds__(256) void check_spans_kernel(const uint64_t* __restrict__ offsets,
+                                                          const uint32_t* __restrict__ lengths,
+                                                          uint64_t count, uint64_t base_bytes,
+                                                          uint32_t extra,
+                                                          unsigned long long* result) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  unsigned long long bad = 0, first = ~0ull;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
+       i += step) {
+    const uint64_t o = offsets[i];
+    const uint64_t need = static_cast<uint64_t>(lengths[i]) + extra;
+    if (o > base_bytes || need > base_bytes - o) {
+      ++bad;
+      first = first < i ? first : i;
+    }
+  }
+  // wave reduction (64 lanes), then one atomic pair per wave
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) {
+    bad += __shfl_xor(bad, k, 64);
+    const unsigned long long f = __shfl_xor(first, k, 64);
+    first = first < f ? first : f;
+  }
+  if ((threadIdx.x & 63u) == 0u && bad) {
+    atomicAdd(result, bad);
+    atomicMin(result + 1, first);
   }
 }
 

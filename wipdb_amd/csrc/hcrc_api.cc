@@ -49,6 +49,8 @@ __global__ void crc32c_lds_partition_kernel(const uint8_t*, const uint64_t*, con
 namespace util {
 __global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*, uint64_t);
 __global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
+__global__ void check_spans_kernel(const uint64_t*, const uint32_t*, uint64_t, uint64_t, uint32_t,
+                                   unsigned long long*);
 }  // namespace util
 }  // namespace wipdb
 
@@ -588,6 +590,7 @@ const char* hcrc_strerror(int code) {
     case HCRC_ERR_HIP: return "HIP runtime error";
     case HCRC_ERR_LAUNCH: return "kernel launch failed";
     case HCRC_ERR_MISMATCH: return "checksum mismatch";
+    case HCRC_ERR_BOUNDS: return "span outside the base buffer";
     default: return "unknown error";
   }
 }
@@ -760,6 +763,43 @@ int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride, ui
                      static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(d_base), stride,
                      length, d_out, static_cast<uint64_t>(count));
   return Launched();
+}
+
+int hcrc_check_spans_async(hcrc_ctx* ctx, uint64_t base_bytes, const uint64_t* d_offsets,
+                           const uint32_t* d_lengths, uint32_t extra, size_t count,
+                           uint64_t* d_result, void* stream) {
+  if (!ctx || !d_result || (count && (!d_offsets || !d_lengths))) return HCRC_ERR_INVALID;
+  HCRC_DEVICE(ctx);
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint64_t init[2] = {0, ~uint64_t(0)};
+  HCRC_CHECK(hipMemcpyAsync(d_result, init, sizeof(init), hipMemcpyHostToDevice, st));
+  if (count == 0) return HCRC_OK;
+  const int grid =
+      static_cast<int>(std::min<uint64_t>((count + 255) / 256, uint64_t(ctx->num_cu) * 8));
+  hipLaunchKernelGGL(wipdb::util::check_spans_kernel, dim3(grid), dim3(256), 0, st, d_offsets,
+                     d_lengths, static_cast<uint64_t>(count), base_bytes, extra,
+                     reinterpret_cast<unsigned long long*>(d_result));
+  return Launched();
+}
+
+int hcrc_check_spans(hcrc_ctx* ctx, uint64_t base_bytes, const uint64_t* d_offsets,
+                     const uint32_t* d_lengths, uint32_t extra, size_t count,
+                     uint64_t* first_bad) {
+  if (!ctx) return HCRC_ERR_INVALID;
+  HCRC_DEVICE(ctx);
+  uint64_t* d_res = nullptr;
+  const hipStream_t st = ctx->stream;
+  HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&d_res), 16, ctx->scratch_pool, st));
+  uint64_t res[2] = {0, ~uint64_t(0)};
+  int rc = hcrc_check_spans_async(ctx, base_bytes, d_offsets, d_lengths, extra, count, d_res, st);
+  if (rc == HCRC_OK &&
+      hipMemcpyAsync(res, d_res, sizeof(res), hipMemcpyDeviceToHost, st) != hipSuccess)
+    rc = HCRC_ERR_HIP;
+  if (hipFreeAsync(d_res, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
+  if (hipStreamSynchronize(st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
+  if (rc) return rc;
+  if (first_bad) *first_bad = res[1];
+  return res[0] ? HCRC_ERR_BOUNDS : HCRC_OK;
 }
 
 int hcrc_fill_splitmix64_async(hcrc_ctx* ctx, void* d_dst, uint64_t nbytes, uint64_t seed,
