@@ -2,7 +2,9 @@
 """Kernel time of the descriptor batch on synthetic span shapes (1 M spans
 each unless noted): which part of a span's shape costs time -- the head
 (unaligned start), the tail (length % 16), the piece (chunks past 256).
-Prints one JSON line per shape; checks a sample against the CPU path."""
+Prints one JSON line per shape; checks a sample against the CPU path.
+--verify: the same byte footprints through the verify kernel (handle size
+n = length - 5: contents + type byte + stored crc = length bytes read)."""
 import json
 import os
 import sys
@@ -36,7 +38,9 @@ SHAPES = [  # name, start offset in slot, length, slot stride
 
 
 def main():
-    only = sys.argv[1] if len(sys.argv) > 1 else ""
+    args = [a for a in sys.argv[1:] if a != "--verify"]
+    verify = "--verify" in sys.argv[1:]
+    only = args[0] if args else ""
     d = torch.device("cuda", 0)
     st = torch.cuda.current_stream(d)
     n = 1 << 20
@@ -50,6 +54,16 @@ def main():
                 continue
             offs = (np.arange(n, dtype=np.uint64) * stride + h).astype(np.uint64)
             lens = np.full(n, ln, np.uint32)
+            if verify:
+                # timing only: the trailers are random, so the statuses are too
+                dl = dev(np.full(n, ln - 5, np.uint32), d)
+                do = dev(offs, d)
+                st8 = torch.empty(n, dtype=torch.uint8, device=d)
+                t = time_kernel(lambda: eng.verify_device(buf, do, dl, st8, stream=st.cuda_stream),
+                                st, 20)
+                print(json.dumps({"shape": name, "verify": True, "ms": round(t * 1e3, 4),
+                                  "GiBps": round(float(lens.sum()) / t / 2**30, 1)}), flush=True)
+                continue
             do, dl = dev(offs, d), dev(lens, d)
             out = torch.empty(n, dtype=torch.int32, device=d)
             t = time_kernel(lambda: eng.batch_device(buf, do, dl, None, out, stream=st.cuda_stream), st, 20)

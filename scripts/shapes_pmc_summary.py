@@ -8,12 +8,13 @@ import json
 import sys
 
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+kern = sys.argv[2] if len(sys.argv) > 2 else "spans_kernel"
 rows = []
 for f in glob.glob(f"{d}/shapes_pmc/**/*counter_collection.csv", recursive=True):
     rows += list(csv.DictReader(open(f)))
 by = collections.defaultdict(dict)
 for r in rows:
-    if "spans_kernel" in r["Kernel_Name"]:
+    if kern in r["Kernel_Name"]:
         by[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
 ids = sorted(by)
 shapes = [json.loads(x) for x in open(f"{d}/shapes.log") if x.startswith("{")]

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -421,6 +422,73 @@ int AutoSplit(const uint8_t* base, const uint64_t* offsets, const uint32_t* leng
   return hits >= kAutoSplitMin ? HCRC_SPLIT_SMALL : 0;
 }
 
+// Persistent helper threads for the pageable -> pinned staging copy (the
+// bound of host batches from pageable memory): spawning threads per piece
+// cost a visible share of each 32 MiB piece.  One Run at a time uses the
+// pool; a concurrent caller (another lane) copies on its own thread instead.
+// Never destroyed (no exit-order hazard with other static destructors).
+class CopyPool {
+ public:
+  static CopyPool& Get() {
+    static CopyPool* p = new CopyPool;
+    return *p;
+  }
+  // fn(a, b) over [0, n) in parts, the caller running one of them
+  void Run(size_t n, const std::function<void(size_t, size_t)>& fn) {
+    std::unique_lock<std::mutex> run(run_mu_, std::try_to_lock);
+    if (!run.owns_lock() || workers_.empty()) {
+      fn(0, n);
+      return;
+    }
+    const size_t parts = workers_.size() + 1, per = (n + parts - 1) / parts;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      per_ = per;
+      pending_ = workers_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0, std::min(n, per));
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  CopyPool() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nt = std::min(7u, hw > 1 ? hw - 1 : 0u);
+    for (unsigned t = 0; t < nt; ++t) workers_.emplace_back([this, t] { Loop(t + 1); });
+    for (auto& w : workers_) w.detach();
+  }
+  void Loop(size_t part) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(size_t, size_t)>* fn;
+      size_t a, b;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        fn = fn_;
+        a = std::min(n_, per_ * part);
+        b = std::min(n_, a + per_);
+      }
+      if (a < b) (*fn)(a, b);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(size_t, size_t)>* fn_ = nullptr;
+  size_t n_ = 0, per_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
 // Copy spans [lo, hi) into a slot's pinned buffer, keeping each span's
 // address mod 16 (so aligned blocks stay on the aligned fast path and the
 // size classes are the caller's).
@@ -436,24 +504,13 @@ void PackSpans(Slot& s, const uint8_t* base, const uint64_t* offsets, const uint
     cur += lengths[i];
   }
   *used_bytes = cur;
-  // the byte copy itself, split over a few threads for big pieces
+  // the byte copy itself, split over the copy pool for big pieces
   const size_t n = hi - lo;
   auto copy = [&](size_t a, size_t b) {
     for (size_t i = a; i < b; ++i) memcpy(s.h_data + s.h_off[i], base + offsets[lo + i], s.h_len[i]);
   };
-  if (cur < (size_t(8) << 20) || n < 64) {
-    copy(0, n);
-  } else {
-    const int nt = 8;
-    std::vector<std::thread> pool;
-    const size_t per = (n + nt - 1) / nt;
-    for (int t = 0; t < nt; ++t) {
-      const size_t a = per * t, b = std::min(n, a + per);
-      if (a >= b) break;
-      pool.emplace_back(copy, a, b);
-    }
-    for (auto& th : pool) th.join();
-  }
+  if (cur < (size_t(4) << 20) || n < 64) copy(0, n);
+  else CopyPool::Get().Run(n, copy);
 }
 
 // Zero-copy: the kernel reads the spans straight out of mapped host memory
