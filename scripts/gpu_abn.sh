@@ -18,7 +18,7 @@ for r in $(seq 1 "$ROUNDS"); do
     e=""
     if [ -n "$WHAT" ] && [ "$WHAT" != none ]; then
       timeout -k 10 200 python scripts/bench_extra.py --what "$WHAT" > gpurun_out/ab_extra.log 2>&1 || exit $?
-      e=$(grep -o '"ms": [0-9.]*\|"kernel_ms": [0-9.]*' gpurun_out/ab_extra.log | tr '\n' ' ')
+      e=$(grep -o '"ms": [0-9.]*\|"kernel_ms": [0-9.]*\|"GiBps_end_to_end": [0-9.]*' gpurun_out/ab_extra.log | tr '\n' ' ')
     fi
     echo "round $r $v: headline $b | $e"
   done
