@@ -353,7 +353,10 @@ __device__ __forceinline__ void load_image(const uint8_t* image, uint32_t w, uin
 // for at first use).
 // ---------------------------------------------------------------------------
 
-// Descriptor batch: span i = base + offsets[i], lengths[i] (+ extra) bytes.
+// Descriptor batch: span i = base + offsets[i], lengths[i] (+ extra) bytes;
+// kInit: an init column (else every init is 0 -- one pointer and one scalar
+// load per span fewer for the batches that have none, e.g. WriteRawBlock's).
+template <bool kInit>
 struct DescSrc {
   const uint8_t* base;
   const uint64_t* off;
@@ -362,7 +365,7 @@ struct DescSrc {
   uint64_t count;
   uint32_t extra;  // verify: +1 type byte
   __device__ __forceinline__ SpanD get(uint64_t s) const {
-    return SpanD{off[s], len[s] + extra, init ? init[s] : 0u, 0u, s};
+    return SpanD{off[s], len[s] + extra, kInit ? init[s] : 0u, 0u, s};
   }
 };
 
@@ -1055,14 +1058,22 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
-// Descriptor batch: out[i] = Extend(inits[i], base + offsets[i], lengths[i]).
+// Descriptor batch: out[i] = Extend(inits[i], base + offsets[i], lengths[i]);
+// INIT = 0: no init column (all 0).
+template <int INIT>
 __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
-  const DescSrc src{base, offsets, lengths, inits, count, 0u};
+  const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u};
   run_ea<0>(src, out, flags, image);
 }
+template __global__ void crc32c_lds_spans_kernel<0>(const uint8_t*, const uint64_t*,
+                                                    const uint32_t*, const uint32_t*, uint32_t*,
+                                                    uint64_t, uint32_t, const uint8_t*);
+template __global__ void crc32c_lds_spans_kernel<1>(const uint8_t*, const uint64_t*,
+                                                    const uint32_t*, const uint32_t*, uint32_t*,
+                                                    uint64_t, uint32_t, const uint8_t*);
 
 // Fixed-size blocks at a fixed stride.
 __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
@@ -1079,7 +1090,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
     const uint8_t* __restrict__ image) {
-  const DescSrc src{base, offsets, lengths, nullptr, count, 1u};
+  const DescSrc<false> src{base, offsets, lengths, nullptr, count, 1u};
   run_ea<1>(src, status, 0u, image);
 }
 

@@ -32,6 +32,7 @@
 
 namespace wipdb {
 namespace lk {
+template <int INIT>
 __global__ void crc32c_lds_spans_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                         const uint32_t*, uint32_t*, uint64_t, uint32_t,
                                         const uint8_t*);
@@ -393,7 +394,8 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
       rc = LaunchClasses(ctx, static_cast<const uint8_t*>(base), off + pos, len + pos,
                          init ? init + pos : nullptr, out + pos, n, 0, mask, st);
     } else {
-      hipLaunchKernelGGL(lk::crc32c_lds_spans_kernel, dim3(LdsGrid(ctx, n)), dim3(lk::kThreads),
+      hipLaunchKernelGGL(init ? lk::crc32c_lds_spans_kernel<1> : lk::crc32c_lds_spans_kernel<0>,
+                         dim3(LdsGrid(ctx, n)), dim3(lk::kThreads),
                          lk::kLdsBytes, st, static_cast<const uint8_t*>(base), off + pos,
                          len + pos, init ? init + pos : nullptr, out + pos,
                          static_cast<uint64_t>(n), mask ? lk::kFlagMask : 0u, ctx->d_image);
@@ -500,7 +502,7 @@ void PackSpans(Slot& s, const uint8_t* base, const uint64_t* offsets, const uint
     cur = ((cur + 15) & ~size_t(15)) + (reinterpret_cast<uintptr_t>(src) & 15);
     s.h_off[i - lo] = cur;
     s.h_len[i - lo] = lengths[i];
-    s.h_init[i - lo] = inits ? inits[i] : 0u;
+    if (inits) s.h_init[i - lo] = inits[i];
     cur += lengths[i];
   }
   *used_bytes = cur;
@@ -530,11 +532,10 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     memcpy(s.h_off, offsets + i, n * 8);
     memcpy(s.h_len, lengths + i, n * 4);
     if (inits) memcpy(s.h_init, inits + i, n * 4);
-    else memset(s.h_init, 0, n * 4);
     HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
     HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
-    HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
-    rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, s.d_init, s.d_out, n,
+    if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
+    rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
                      flags | AutoSplit(host_base, offsets + i, lengths + i, n), st);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
@@ -581,8 +582,8 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     HCRC_CHECK(hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, st));
     HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
     HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
-    HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
-    rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, s.d_init, s.d_out, n,
+    if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
+    rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
                      flags | AutoSplit(base, offsets + i, lengths + i, n), st);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
@@ -675,7 +676,8 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
     HCRC_CHECK(hipMemPoolSetAttribute(ctx->scratch_pool, hipMemPoolAttrReleaseThreshold, &keep));
   }
   const void* kernels[] = {
-      reinterpret_cast<const void*>(lk::crc32c_lds_spans_kernel),
+      reinterpret_cast<const void*>(lk::crc32c_lds_spans_kernel<0>),
+      reinterpret_cast<const void*>(lk::crc32c_lds_spans_kernel<1>),
       reinterpret_cast<const void*>(lk::crc32c_lds_strided_kernel),
       reinterpret_cast<const void*>(lk::crc32c_lds_verify_kernel),
       reinterpret_cast<const void*>(lk::crc32c_lds_list_kernel<1, 0>),
