@@ -1,4 +1,5 @@
-"""World-size-2 (gloo, CPU) coverage of the multi-GPU path.
+"""World-size-2 and -8 (gloo, CPU) coverage of the multi-GPU path (SURVEY.md 8e;
+world size 8 rehearses the driver's 8-GPU launch: 8 ranks, one shard each).
 
 The path shards with no data-path collective: each rank owns a contiguous
 range of blocks (weak scaling, bench.py) or a byte-balanced range of spans
@@ -89,11 +90,12 @@ def _worker(rank: int, world: int, port: int, blocks: int, outdir: str):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(300)
-def test_gloo_world2_shards(tmp_path, oracle):
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_world_shards(tmp_path, oracle, world):
     import torch.multiprocessing as mp
     from tests.golden.common import splitmix64_bytes
-    blocks, world = 96, 2
+    blocks = 96
     mp.spawn(_worker, args=(world, _free_port(), blocks, str(tmp_path)), nprocs=world, join=True)
     got = np.load(tmp_path / "blocks.npy")
     full = splitmix64_bytes(SEED, world * blocks * BLOCK)
