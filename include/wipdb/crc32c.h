@@ -30,6 +30,10 @@ namespace crc32c {
 
 enum class BatchPolicy { kAuto = 0, kGpuOnly = 1, kCpuOnly = 2 };
 
+// The device argument's default: the devices listed in WIPDB_CRC_DEVICES
+// (below), else device 0.
+constexpr int kDeviceFromEnv = -1;
+
 struct BatchStats {
   uint64_t gpu_batches = 0;
   uint64_t cpu_batches = 0;  // kAuto batches that ran on the host
@@ -39,12 +43,25 @@ struct BatchStats {
 // out[i] = Extend(inits ? inits[i] : 0, base + offsets[i], lengths[i]),
 // Mask()-ed when mask is true.  Host memory.  Returns 0 or an HCRC_ERR_*
 // code (only possible under kGpuOnly).
+//
+// Runtime selection without recompiling the caller (read once per process):
+//   WIPDB_CRC_MODE=auto|gpu|cpu   what kAuto means: the size threshold
+//                                  below (default), every batch on the GPU
+//                                  (still falling back to the host if no
+//                                  device works), or every batch on the host
+//   WIPDB_CRC_MIN_GPU_BATCH=N     kAuto's threshold (default 64 spans)
+//   WIPDB_CRC_DEVICES=0,1,...     devices for device == kDeviceFromEnv:
+//                                  calls are spread round robin over them, and
+//                                  a batch of >= 8192 spans is sharded over
+//                                  all of them by bytes (hcrc_batch_multi)
 int ExtendBatch(const char* base, const uint64_t* offsets,
                 const uint32_t* lengths, const uint32_t* inits, uint32_t* out,
                 size_t count, bool mask,
-                BatchPolicy policy = BatchPolicy::kAuto, int device = 0);
+                BatchPolicy policy = BatchPolicy::kAuto,
+                int device = kDeviceFromEnv);
 
-// Below this many spans kAuto stays on the CPU (a launch costs more).
+// Below this many spans kAuto stays on the CPU (a launch costs more);
+// overrides WIPDB_CRC_MIN_GPU_BATCH.
 void SetMinGpuBatch(size_t spans);
 BatchStats GetBatchStats();
 

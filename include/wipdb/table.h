@@ -89,7 +89,8 @@ struct TableOptions {
   int bloom_bits_per_key = 0;        // 0: no filter policy; else NewBloomFilterPolicy(bits)
   size_t max_buffer_size = 4u << 20; // EnvOptions::writable_file_max_buffer_size (env.h:85)
   CrcMode crc_mode = CrcMode::kBatchAuto;
-  int device = 0;                    // HIP device for the batched modes
+  int device = -1;                   // HIP device for the batched modes; -1: WIPDB_CRC_DEVICES, else 0
+                                     // (wipdb::crc32c::kDeviceFromEnv)
   const Comparator* comparator = nullptr;  // nullptr: BytewiseComparator()
   FilterKeys filter_keys = FilterKeys::kWholeKey;
   // kBatchGpu / kBatchAuto: the write buffer is pinned host memory (pooled),
@@ -198,7 +199,7 @@ class CompactionInput {
     bool verify_checksums = true;            // Options::paranoid_checks
     size_t prefetch_blocks = 64;             // per input and CRC batch
     CrcMode crc_mode = CrcMode::kBatchAuto;
-    int device = 0;
+    int device = -1;  // -1: WIPDB_CRC_DEVICES, else 0 (crc32c::kDeviceFromEnv)
   };
   // The images must outlive the reader (an mmap'd file, or pinned memory for
   // zero-copy batches).

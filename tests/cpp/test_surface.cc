@@ -62,7 +62,10 @@ static uint32_t RdbMask(uint32_t c) { return rocksdb::crc32c::Mask(c); }
 static uint32_t RdbUnmask(uint32_t c) { return rocksdb::crc32c::Unmask(c); }
 
 int main(int argc, char** argv) {
-  const bool expect_gpu = argc > 1 && atoi(argv[1]) != 0;
+  // argv[1]: 0 = no device, 1 = a device, 2 = a device + WIPDB_CRC_MODE=cpu,
+  // 3 = a device + WIPDB_CRC_DEVICES=0,0
+  const int mode = argc > 1 ? atoi(argv[1]) : 0;
+  const bool expect_gpu = mode != 0;
   StandardResults<KvExtend, KvMask, KvUnmask>();
   StandardResults<LdbExtend, LdbMask, LdbUnmask>();
   StandardResults<RdbExtend, RdbMask, RdbUnmask>();
@@ -100,7 +103,35 @@ int main(int argc, char** argv) {
            0);
   for (size_t i = 0; i < off.size(); ++i) CHECK_EQ(got[i], want[i]);
   auto st = wipdb::crc32c::GetBatchStats();
-  if (expect_gpu) {
+  if (mode == 2) {
+    // GPU present, WIPDB_CRC_MODE=cpu: kAuto stays on the host, kGpuOnly
+    // still reaches the device
+    CHECK_EQ(st.cpu_batches, 2);
+    CHECK_EQ(st.gpu_batches, 0);
+    std::fill(got.begin(), got.end(), 0u);
+    CHECK_EQ(wipdb::crc32c::ExtendBatch(file.data(), off.data(), len.data(), nullptr,
+                                        got.data(), off.size(), true, BatchPolicy::kGpuOnly),
+             0);
+    for (size_t i = 0; i < off.size(); ++i) CHECK_EQ(got[i], want[i]);
+    CHECK_EQ(wipdb::crc32c::GetBatchStats().gpu_batches, 1);
+  } else if (mode == 3) {
+    // GPU present, WIPDB_CRC_DEVICES lists device 0 twice: a batch of
+    // >= 8192 spans is sharded over the list (hcrc_batch_multi)
+    CHECK_EQ(st.gpu_batches, 1);
+    std::vector<uint64_t> o2;
+    std::vector<uint32_t> l2, w2, g2;
+    for (int r = 0; r < 40; ++r)
+      for (size_t i = 0; i < off.size(); ++i) {
+        o2.push_back(off[i]);
+        l2.push_back(len[i]);
+        w2.push_back(want[i]);
+      }
+    g2.assign(o2.size(), 0u);
+    CHECK_EQ(wipdb::crc32c::ExtendBatch(file.data(), o2.data(), l2.data(), nullptr, g2.data(),
+                                        o2.size(), true, BatchPolicy::kGpuOnly),
+             0);
+    for (size_t i = 0; i < o2.size(); ++i) CHECK_EQ(g2[i], w2[i]);
+  } else if (expect_gpu) {
     CHECK_EQ(st.gpu_batches, 1);
     std::fill(got.begin(), got.end(), 0u);
     CHECK_EQ(wipdb::crc32c::ExtendBatch(file.data(), off.data(), len.data(), nullptr,

@@ -80,6 +80,12 @@ def test_cpp_surface_drop_in_cpu(tmp_path):
     r = subprocess.run([exe, "0"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
+    # the runtime selector: WIPDB_CRC_MODE=cpu, a device list, a threshold --
+    # without a device every kAuto batch still lands on the host
+    env = dict(os.environ, WIPDB_CRC_MODE="cpu", WIPDB_CRC_DEVICES="0,1",
+               WIPDB_CRC_MIN_GPU_BATCH="1")
+    r = subprocess.run([exe, "0"], capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 def test_kernel_span_geometry_host(tmp_path):

@@ -550,6 +550,14 @@ def test_cpp_surface_drop_in_gpu(tmp_path):
                     "-lhip_crc32c_batch", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
     r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+    # the runtime selector (include/wipdb/crc32c.h): WIPDB_CRC_MODE=cpu keeps
+    # kAuto on the host; WIPDB_CRC_DEVICES shards big batches over the list
+    env = dict(os.environ, WIPDB_CRC_MODE="cpu")
+    r = subprocess.run([exe, "2"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    env = dict(os.environ, WIPDB_CRC_DEVICES="0,0")
+    r = subprocess.run([exe, "3"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 def test_concurrent_host_batches_share_a_context(engine, oracle):

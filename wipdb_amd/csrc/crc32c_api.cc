@@ -10,9 +10,12 @@
 // rocksdb/util/crc32c.cc's.
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/hip_crc32c_batch.h"
 #include "../../include/wipdb/crc32c.h"
@@ -67,13 +70,51 @@ namespace wipdb {
 namespace crc32c {
 
 namespace {
-std::atomic<size_t> g_min_gpu_batch{64};
+constexpr size_t kDefaultMinGpuBatch = 64;
+constexpr size_t kMultiMinSpans = 8192;  // a listed-devices batch this big is sharded
+constexpr size_t kUnset = ~size_t(0);
+std::atomic<size_t> g_min_gpu_batch{kUnset};  // SetMinGpuBatch, else the env / default
 std::atomic<uint64_t> g_gpu_batches{0}, g_cpu_batches{0};
 std::atomic<int> g_last_error{0};
+std::atomic<uint32_t> g_round_robin{0};
 std::mutex g_mu;
 hcrc_ctx* g_ctx[64] = {nullptr};
 int g_ctx_rc[64] = {0};
 bool g_ctx_tried[64] = {false};
+
+// WIPDB_CRC_* (include/wipdb/crc32c.h), read once.
+struct EnvConfig {
+  enum Mode { kAuto, kGpu, kCpu } mode = kAuto;
+  size_t min_batch = kDefaultMinGpuBatch;
+  std::vector<int> devices;
+};
+const EnvConfig& Env() {
+  static const EnvConfig cfg = [] {
+    EnvConfig c;
+    if (const char* m = getenv("WIPDB_CRC_MODE")) {
+      const std::string v(m);
+      if (v == "gpu") c.mode = EnvConfig::kGpu;
+      else if (v == "cpu") c.mode = EnvConfig::kCpu;
+    }
+    if (const char* n = getenv("WIPDB_CRC_MIN_GPU_BATCH")) {
+      char* end = nullptr;
+      const unsigned long long v = strtoull(n, &end, 10);
+      if (end != n && *end == '\0') c.min_batch = static_cast<size_t>(v);
+    }
+    if (const char* d = getenv("WIPDB_CRC_DEVICES")) {
+      const char* p = d;
+      while (*p) {
+        char* end = nullptr;
+        const long v = strtol(p, &end, 10);
+        if (end == p) break;  // not a number: ignore the rest
+        if (v >= 0 && v < 64) c.devices.push_back(static_cast<int>(v));
+        p = *end == ',' ? end + 1 : end;
+      }
+    }
+    return c;
+  }();
+  return cfg;
+}
 
 int CtxFor(int device, hcrc_ctx** out) {
   if (device < 0 || device >= 64) return HCRC_ERR_NO_DEVICE;
@@ -85,18 +126,38 @@ int CtxFor(int device, hcrc_ctx** out) {
   *out = g_ctx[device];
   return g_ctx_rc[device];
 }
+
+int GpuBatch(const char* base, const uint64_t* offsets, const uint32_t* lengths,
+             const uint32_t* inits, uint32_t* out, size_t count, int flags, int device) {
+  const EnvConfig& env = Env();
+  if (device == kDeviceFromEnv) {
+    const size_t nd = env.devices.size();
+    if (nd > 1 && count >= kMultiMinSpans)
+      return hcrc_batch_multi(env.devices.data(), static_cast<int>(nd), base, offsets, lengths,
+                              inits, out, count, flags);
+    device = nd ? env.devices[g_round_robin.fetch_add(1) % nd] : 0;
+  }
+  hcrc_ctx* ctx = nullptr;
+  int rc = CtxFor(device, &ctx);
+  if (rc == HCRC_OK) rc = hcrc_batch(ctx, base, offsets, lengths, inits, out, count, flags);
+  return rc;
+}
 }  // namespace
 
 int ExtendBatch(const char* base, const uint64_t* offsets, const uint32_t* lengths,
                 const uint32_t* inits, uint32_t* out, size_t count, bool mask,
                 BatchPolicy policy, int device) {
   const int flags = mask ? HCRC_MASK_OUTPUT : 0;
+  const EnvConfig& env = Env();
+  size_t min_batch = g_min_gpu_batch.load();
+  if (min_batch == kUnset) min_batch = env.min_batch;
+  if (policy == BatchPolicy::kAuto) {
+    if (env.mode == EnvConfig::kCpu) policy = BatchPolicy::kCpuOnly;
+    else if (env.mode == EnvConfig::kGpu) min_batch = 0;
+  }
   if (policy != BatchPolicy::kCpuOnly &&
-      (policy == BatchPolicy::kGpuOnly || count >= g_min_gpu_batch.load())) {
-    hcrc_ctx* ctx = nullptr;
-    int rc = CtxFor(device, &ctx);
-    if (rc == HCRC_OK)
-      rc = hcrc_batch(ctx, base, offsets, lengths, inits, out, count, flags);
+      (policy == BatchPolicy::kGpuOnly || count >= min_batch)) {
+    const int rc = GpuBatch(base, offsets, lengths, inits, out, count, flags, device);
     if (rc == HCRC_OK) {
       ++g_gpu_batches;
       return HCRC_OK;
