@@ -265,6 +265,27 @@ def test_fast_path_shapes_crc_and_verify(engine, oracle):
     np.testing.assert_array_equal(st.cpu().numpy(), expect)
 
 
+def test_host_batch_long_spans_split(engine, oracle):
+    """Host batches cut spans of >= 256 KiB into 64 KiB parts run on many
+    waves and combined on the host by linearity (hcrc_api.cc BatchHostLong):
+    every length around the cut and part boundaries, odd offsets, inits and
+    masked output, mixed with short spans -- against the oracle."""
+    rng = np.random.default_rng(262144)
+    buf = rng.integers(0, 256, 9 << 20, dtype=np.uint8)
+    K = 1 << 10
+    lens = [256 * K - 1, 256 * K, 256 * K + 1, 320 * K, 320 * K + 3, (1 << 20) + 17,
+            (3 << 20) + 5, 4 * 64 * K + 64 * K - 1, 100, 4096, 70000, 0, 1, 255 * K]
+    lens = np.array(rng.permutation(lens * 3), np.uint32)
+    offs = np.array([int(rng.integers(0, buf.size - int(n) - 1)) for n in lens], np.uint64)
+    inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    inits[::4] = 0
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(engine.batch(buf, offs, lens, inits), want)
+    np.testing.assert_array_equal(engine.batch(buf, offs, lens, inits, mask_output=True),
+                                  np.array([oracle.lib.oracle_mask(int(x)) for x in want], np.uint32))
+    np.testing.assert_array_equal(engine.batch(buf, offs, lens), oracle.batch(buf, offs, lens))
+
+
 def test_check_spans_bounds(engine):
     """hcrc_check_spans: the count and lowest index of spans that leave the
     base buffer, overflow-safe, for CRC (extra 0) and verify (extra 5)

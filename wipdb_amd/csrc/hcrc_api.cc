@@ -600,6 +600,83 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
   return HCRC_OK;
 }
 
+// Long spans of a host batch (SURVEY 5's long-context analogue): a span of
+// at least kLongSpan bytes runs as parts of kPartBytes (the first part takes
+// the remainder), so its segments run on many waves at once instead of one
+// chained wave; the parts' CRCs are combined on the host by linearity
+// (gf2_crc32c.h): part 0 runs with the span's init, the others from init ~0
+// (so they return ~feed(0, part)), and
+//   feed(~init, span) = Horner over r = shift(r, kPartBytes) ^ feed(0, part j),
+// the same identity crc32c_3way's CombineCRC uses (kv/src/util/crc32c.cc:640-657).
+constexpr uint64_t kPartBytes = uint64_t(64) << 10;
+constexpr uint64_t kLongSpan = 4 * kPartBytes;
+
+struct PartShift {
+  uint32_t t[4][256];
+  PartShift() { wipdb::gf2::BuildShiftTable(kPartBytes, t); }
+  uint32_t operator()(uint32_t r) const {
+    return t[0][r & 0xffu] ^ t[1][(r >> 8) & 0xffu] ^ t[2][(r >> 16) & 0xffu] ^ t[3][r >> 24];
+  }
+};
+
+int BatchHostLong(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
+                  const uint32_t* lengths, const uint32_t* inits, uint32_t* out, size_t count,
+                  int flags) {
+  size_t parts = 0;
+  bool any = false;
+  for (size_t i = 0; i < count; ++i) {
+    if (lengths[i] >= kLongSpan) {
+      any = true;
+      parts += (lengths[i] + kPartBytes - 1) / kPartBytes;
+    } else {
+      ++parts;
+    }
+  }
+  if (!any) return BatchHost(ctx, base, offsets, lengths, inits, out, count, flags);
+  std::vector<uint64_t> po(parts);
+  std::vector<uint32_t> pl(parts), pi(parts), pr(parts);
+  size_t k = 0;
+  for (size_t i = 0; i < count; ++i) {
+    const uint32_t init = inits ? inits[i] : 0u;
+    const uint64_t n = lengths[i];
+    if (n < kLongSpan) {
+      po[k] = offsets[i];
+      pl[k] = static_cast<uint32_t>(n);
+      pi[k++] = init;
+      continue;
+    }
+    const uint64_t m = (n + kPartBytes - 1) / kPartBytes;
+    const uint64_t first = n - (m - 1) * kPartBytes;  // 1 .. kPartBytes
+    po[k] = offsets[i];
+    pl[k] = static_cast<uint32_t>(first);
+    pi[k++] = init;
+    for (uint64_t j = 1; j < m; ++j) {
+      po[k] = offsets[i] + first + (j - 1) * kPartBytes;
+      pl[k] = static_cast<uint32_t>(kPartBytes);
+      pi[k++] = ~0u;
+    }
+  }
+  const int rc = BatchHost(ctx, base, po.data(), pl.data(), pi.data(), pr.data(), parts,
+                           flags & ~HCRC_MASK_OUTPUT);
+  if (rc) return rc;
+  static const PartShift shift;
+  const bool mask = (flags & HCRC_MASK_OUTPUT) != 0;
+  k = 0;
+  for (size_t i = 0; i < count; ++i) {
+    uint32_t v;
+    if (lengths[i] < kLongSpan) {
+      v = pr[k++];
+    } else {
+      const uint64_t m = (uint64_t(lengths[i]) + kPartBytes - 1) / kPartBytes;
+      uint32_t r = ~pr[k++];
+      for (uint64_t j = 1; j < m; ++j) r = shift(r) ^ ~pr[k++];
+      v = ~r;
+    }
+    out[i] = mask ? wipdb::gf2::Mask(v) : v;
+  }
+  return HCRC_OK;
+}
+
 std::mutex g_ctx_mu;
 std::map<int, hcrc_ctx*>& SharedCtxs() {
   static auto* m = new std::map<int, hcrc_ctx*>;
@@ -743,8 +820,8 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const u
     HCRC_CHECK(hipStreamSynchronize(lane->stream));
     return HCRC_OK;
   }
-  return BatchHost(ctx, static_cast<const uint8_t*>(base), offsets, lengths, init_crcs, out_crcs,
-                   count, flags);
+  return BatchHostLong(ctx, static_cast<const uint8_t*>(base), offsets, lengths, init_crcs,
+                       out_crcs, count, flags);
 }
 
 int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
