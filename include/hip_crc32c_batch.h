@@ -83,6 +83,17 @@ extern "C" {
  * blocks).  hcrc_batch on host memory chooses it by itself.  Uses
  * stream-ordered scratch (~60 bytes per span). */
 #define HCRC_SPLIT_SMALL 0x4
+/* Long spans (device batches; host batches do it by themselves for spans of
+ * >= 256 KiB): a span of >= 128 KiB is cut into 16 KiB parts checksummed on
+ * many waves at once and combined by GF(2) linearity (crc32c_3way's
+ * CombineCRC, kv/src/util/crc32c.cc:640-657) -- a lone span otherwise runs
+ * its segments chained on one wave (~2.7 GiB/s).  Same results; four
+ * launches instead of one and stream-ordered scratch (~36 bytes per span +
+ * a pool of 64 Ki..1 Mi parts, past which spans stay whole).  A latency
+ * tool for batches of few long spans (a lone 16 MiB span: 5.6 -> 0.14 ms);
+ * batches of many short spans run slower with it.  Takes precedence over
+ * HCRC_SPLIT_SMALL. */
+#define HCRC_SPLIT_LONG 0x8
 
 typedef struct hcrc_ctx hcrc_ctx;
 

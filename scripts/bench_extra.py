@@ -84,6 +84,7 @@ def check_sample(host, offs, lens, got, rng, k=4000):
 
 
 SPLIT = False  # --split: HCRC_SPLIT_SMALL on the device batches
+SPLIT_LONG = False  # --split-long: HCRC_SPLIT_LONG on config 3's device batches
 
 
 def batch_latency(eng, dbuf, do, dl, stream, nbatch_bytes=2 << 20, reps=200):
@@ -99,7 +100,8 @@ def batch_latency(eng, dbuf, do, dl, stream, nbatch_bytes=2 << 20, reps=200):
         o_i, l_i = do[lo:lo + per], dl[lo:lo + per]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream, split_small=SPLIT)
+        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream, split_small=SPLIT,
+                         split_long=SPLIT_LONG)
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t0)
     lat = np.array(lat[20:]) * 1e6
@@ -112,12 +114,13 @@ def run_mixed(eng, d, stream, rng, gib):
     host = rng.integers(0, 256, nbytes, dtype=np.uint8)
     dbuf = torch.from_numpy(host).to(d)
     res = {"config": "3 mixed (Zipf 0.99, SST-packed, unaligned)", "split_small": SPLIT,
+           "split_long": SPLIT_LONG,
            "buckets": {}}
     offs, lens, L = zipf_spans(rng, nbytes, BUCKETS)
     do, dl = dev(offs, d), dev(lens, d)
     out = torch.empty(offs.size, dtype=torch.int32, device=d)
     t = time_kernel(lambda: eng.batch_device(dbuf, do, dl, None, out, stream=stream.cuda_stream,
-                                                 split_small=SPLIT),
+                                                 split_small=SPLIT, split_long=SPLIT_LONG),
                     stream, 10)
     got = out.cpu().numpy().view(np.uint32)
     res["mixed"] = {"spans": int(offs.size), "bytes": int(lens.sum()),
@@ -129,7 +132,8 @@ def run_mixed(eng, d, stream, rng, gib):
         dob, dlb = dev(ob, d), dev(lb, d)
         outb = torch.empty(ob.size, dtype=torch.int32, device=d)
         tb = time_kernel(lambda: eng.batch_device(dbuf, dob, dlb, None, outb,
-                                                  stream=stream.cuda_stream, split_small=SPLIT),
+                                                  stream=stream.cuda_stream, split_small=SPLIT,
+                                                  split_long=SPLIT_LONG),
                          stream, 10)
         gotb = outb.cpu().numpy().view(np.uint32)
         res["buckets"][str(b)] = {"spans": int(ob.size),
@@ -285,12 +289,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="mixed,sst,host4k")
     ap.add_argument("--split", action="store_true", help="HCRC_SPLIT_SMALL on device batches")
+    ap.add_argument("--split-long", action="store_true",
+                    help="HCRC_SPLIT_LONG on config 3's device batches")
     ap.add_argument("--mixed-gib", type=float, default=2.0)
     ap.add_argument("--ssts", type=int, default=256)
     ap.add_argument("--host-blocks", type=int, default=1 << 18)
     a = ap.parse_args()
-    global SPLIT
+    global SPLIT, SPLIT_LONG
     SPLIT = a.split
+    SPLIT_LONG = a.split_long
     rng = np.random.default_rng(42)
     d = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(d)

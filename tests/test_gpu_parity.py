@@ -286,6 +286,54 @@ def test_host_batch_long_spans_split(engine, oracle):
     np.testing.assert_array_equal(engine.batch(buf, offs, lens), oracle.batch(buf, offs, lens))
 
 
+def test_device_batch_split_long(engine, oracle):
+    """HCRC_SPLIT_LONG: device spans of >= 128 KiB in 16 KiB parts on many
+    waves, combined by linearity (crc32c_util.hip split_* kernels): lengths
+    around the cut and the part edges, odd offsets, inits, masked output,
+    short spans in between, a lone 5 MiB span, a lone span past the smallest
+    part pool (1 GiB + ...: stays whole); and the flag combined with
+    HCRC_SPLIT_SMALL -- against the oracle."""
+    rng = np.random.default_rng(65536)
+    buf = rng.integers(0, 256, 12 << 20, dtype=np.uint8)
+    K = 1 << 10
+    lens = [128 * K - 1, 128 * K, 128 * K + 1, 144 * K, 144 * K + 3, 160 * K - 5, (1 << 20) + 17,
+            (3 << 20) + 5, 100, 4096, 4200, 0, 3, 64 * K, 129 * K + 16 * K]
+    lens = np.array(rng.permutation(lens * 3), np.uint32)
+    offs = np.array([int(rng.integers(0, buf.size - int(n) - 1)) for n in lens], np.uint64)
+    inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    inits[::4] = 0
+    want = oracle.batch(buf, offs, lens, inits)
+    import torch
+    d_buf, d_off, d_len, d_ini = _t(buf), _t(offs), _t(lens), _t(inits)
+    out = engine.batch_device(d_buf, d_off, d_len, d_ini, split_long=True)
+    np.testing.assert_array_equal(_u32(out), want)
+    out = engine.batch_device(d_buf, d_off, d_len, d_ini, mask_output=True, split_long=True,
+                              split_small=True)
+    np.testing.assert_array_equal(_u32(out),
+                                  np.array([oracle.lib.oracle_mask(int(x)) for x in want], np.uint32))
+    out = engine.batch_device(d_buf, d_off, d_len, None, split_long=True)
+    np.testing.assert_array_equal(_u32(out), oracle.batch(buf, offs, lens))
+    one_o, one_l = np.array([7], np.uint64), np.array([(5 << 20) + 11], np.uint32)
+    out = engine.batch_device(d_buf, _t(one_o), _t(one_l), split_long=True)
+    np.testing.assert_array_equal(_u32(out), oracle.batch(buf, one_o, one_l))
+    # 1 GiB + 5 bytes: 65537 parts, one past the pool -> computed whole (and
+    # the long span after it in the same wave finds the pool taken: whole too)
+    nbig = (1 << 30) + (2 << 20)
+    big = torch.zeros(nbig, dtype=torch.uint8, device="cuda:0")
+    big[-(1 << 20):] = d_buf[:1 << 20]
+    bo = np.array([1, nbig - 300000], np.uint64)
+    bl = np.array([(1 << 30) + 5, 290000], np.uint32)
+    out = engine.batch_device(big, _t(bo), _t(bl), split_long=True)
+    host_tail = big[-(1 << 20):].cpu().numpy()
+    want_small = oracle.batch(host_tail, bo[1:] - np.uint64(nbig - host_tail.size), bl[1:])
+    ref_big = engine.batch_device(big, _t(bo[:1]), _t(bl[:1]))  # the unsplit kernel's answer
+    got = _u32(out)
+    assert int(got[1]) == int(want_small[0])
+    assert int(got[0]) == int(_u32(ref_big)[0])
+    del big
+    torch.cuda.synchronize()
+
+
 def test_check_spans_bounds(engine):
     """hcrc_check_spans: the count and lowest index of spans that leave the
     base buffer, overflow-safe, for CRC (extra 0) and verify (extra 5)

@@ -30,6 +30,7 @@ HCRC_HOST_PTRS = 0x0
 HCRC_DEVICE_PTRS = 0x1
 HCRC_MASK_OUTPUT = 0x2
 HCRC_SPLIT_SMALL = 0x4
+HCRC_SPLIT_LONG = 0x8
 
 _c = ctypes
 _u32p = _c.POINTER(_c.c_uint32)

@@ -19,7 +19,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HCRC_SPLIT_SMALL, HcrcError, check
+from ._lib import (HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HCRC_SPLIT_LONG, HCRC_SPLIT_SMALL,
+                   HcrcError, check)
 
 MASK_DELTA = 0xA282EAD8
 
@@ -192,10 +193,11 @@ class Engine:
 
     def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
                      mask_output: bool = False, stream=None, split_small: bool = False,
-                     check_bounds: bool = False):
+                     check_bounds: bool = False, split_long: bool = False):
         """Asynchronous batch on device tensors; returns the uint32 out tensor
         (int32 storage).  Enqueued on ``stream`` (default: torch's current).
-        ``split_small``: HCRC_SPLIT_SMALL (the size classes).  Offsets are
+        ``split_small``: HCRC_SPLIT_SMALL (the size classes); ``split_long``:
+        HCRC_SPLIT_LONG (spans of >= 64 KiB in 16 KiB parts on many waves).  Offsets are
         int64, lengths / inits / out 32-bit, all contiguous on this engine's
         device; ``check_bounds`` also checks every span against base (a
         device kernel and a sync, hcrc_check_spans)."""
@@ -207,6 +209,8 @@ class Engine:
         flags = HCRC_DEVICE_PTRS | (HCRC_MASK_OUTPUT if mask_output else 0)
         if split_small:
             flags |= HCRC_SPLIT_SMALL
+        if split_long:
+            flags |= HCRC_SPLIT_LONG
         check(self._lib.hcrc_batch_async(self._ctx, _ptr(base_t), _ptr(offsets_t), _ptr(lengths_t),
                                          _ptr(inits_t), _ptr(out_t), n, flags,
                                          self._stream_of(stream)), "hcrc_batch_async")

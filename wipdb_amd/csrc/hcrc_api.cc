@@ -53,6 +53,13 @@ __global__ void readstream_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t*,
 __global__ void fill_splitmix64_kernel(uint64_t*, uint64_t, uint64_t, uint64_t);
 __global__ void check_spans_kernel(const uint64_t*, const uint32_t*, uint64_t, uint64_t, uint32_t,
                                    unsigned long long*);
+__global__ void split_expand_kernel(const uint64_t*, const uint32_t*, const uint32_t*, uint64_t,
+                                    uint32_t, uint32_t, uint32_t, uint64_t*, uint32_t*, uint32_t*,
+                                    uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+__global__ void split_copy_kernel(const uint32_t*, const uint32_t*, uint32_t*, uint64_t, uint32_t);
+__global__ void split_combine_kernel(const uint32_t*, const uint32_t*, const uint32_t*,
+                                     const uint32_t*, const uint32_t*, uint32_t*, uint64_t, uint32_t,
+                                     uint32_t, uint32_t);
 }  // namespace util
 }  // namespace wipdb
 
@@ -381,16 +388,77 @@ int LaunchClasses(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const
   return rc;
 }
 
+// Long spans of a device batch (HCRC_SPLIT_LONG, crc32c_util.hip): spans of
+// at least kDevLongSpan bytes run as kDevPartBytes parts on many waves.  An
+// expand pass writes the list (every other span once, the long ones' parts;
+// a pool of `cap` part slots, past which spans stay whole), the class-1 list
+// kernel computes it into a scratch array, then the unsplit results are
+// copied out and each split span's parts combined by one wave.
+constexpr uint32_t kDevPartBytes = 16u << 10;
+constexpr uint32_t kDevLongSpan = 128u << 10;
+constexpr size_t kDevPartCap = size_t(1) << 20;
+constexpr size_t kDevPartCapMin = size_t(1) << 16;  // 1 GiB of long spans in any batch
+
+int LaunchLong(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
+               const uint32_t* init, uint32_t* out, size_t n, bool mask, hipStream_t st) {
+  const size_t cap = std::min(kDevPartCap, std::max(kDevPartCapMin, 16 * n));
+  const size_t E = n + cap;  // list entries / scratch results
+  const size_t bytes = E * 8 + E * 16 + n * 8 + 16;
+  uint8_t* scratch = nullptr;
+  HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), bytes, ctx->scratch_pool,
+                                    st));
+  uint64_t* l_off = reinterpret_cast<uint64_t*>(scratch);
+  uint32_t* l_len = reinterpret_cast<uint32_t*>(scratch + E * 8);
+  uint32_t* l_init = l_len + E;
+  uint32_t* l_id = l_init + E;
+  uint32_t* tmp = l_id + E;
+  uint32_t* first = tmp + E;
+  uint32_t* split_idx = first + n;
+  uint32_t* counters = split_idx + n;
+  int rc = hipMemsetAsync(counters, 0, 16, st) == hipSuccess ? HCRC_OK : HCRC_ERR_HIP;
+  if (rc == HCRC_OK) {
+    const int g = static_cast<int>(std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8));
+    hipLaunchKernelGGL(wipdb::util::split_expand_kernel, dim3(std::max(g, 1)), dim3(256), 0, st,
+                       off, len, init, static_cast<uint64_t>(n), kDevPartBytes, kDevLongSpan,
+                       static_cast<uint32_t>(cap), l_off, l_len, l_init, l_id, first, split_idx,
+                       counters);
+    auto* const list1 = lk::crc32c_lds_list_kernel<1, 0>;
+    hipLaunchKernelGGL(list1, dim3(ctx->num_cu), dim3(lk::kThreads),
+                       lk::kLdsBytes, st, base, static_cast<const uint64_t*>(l_off),
+                       static_cast<const uint32_t*>(l_len), static_cast<const uint32_t*>(l_init),
+                       static_cast<const uint32_t*>(l_id), static_cast<const uint32_t*>(counters),
+                       static_cast<void*>(tmp), 0u, static_cast<const uint8_t*>(ctx->d_image));
+    hipLaunchKernelGGL(wipdb::util::split_copy_kernel, dim3(std::max(g, 1)), dim3(256), 0, st,
+                       static_cast<const uint32_t*>(tmp), static_cast<const uint32_t*>(first), out,
+                       static_cast<uint64_t>(n), mask ? 1u : 0u);
+    hipLaunchKernelGGL(wipdb::util::split_combine_kernel, dim3(ctx->num_cu * 4), dim3(256), 0, st,
+                       len, static_cast<const uint32_t*>(first),
+                       static_cast<const uint32_t*>(split_idx),
+                       static_cast<const uint32_t*>(counters), static_cast<const uint32_t*>(tmp),
+                       out, static_cast<uint64_t>(n), kDevPartBytes,
+                       wipdb::gf2::XPow8N(kDevPartBytes), mask ? 1u : 0u);
+    rc = Launched();
+  }
+  if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
+  return rc;
+}
+
 // Descriptor batch on device memory, enqueued on st.
 int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
                 const uint32_t* init, uint32_t* out, size_t count, int flags, hipStream_t st) {
   const bool mask = (flags & HCRC_MASK_OUTPUT) != 0;
-  const bool split = (flags & HCRC_SPLIT_SMALL) != 0;
-  const size_t piece_max = split ? size_t(lk::kMaxListSpans) : kMaxLaunchSpans;
+  const bool split_long = (flags & HCRC_SPLIT_LONG) != 0;
+  const bool split = !split_long && (flags & HCRC_SPLIT_SMALL) != 0;
+  const size_t piece_max = split_long ? size_t(lk::kMaxListSpans) - kDevPartCap
+                           : split    ? size_t(lk::kMaxListSpans)
+                                      : kMaxLaunchSpans;
   for (size_t pos = 0; pos < count; pos += piece_max) {
     const size_t n = std::min(count - pos, piece_max);
     int rc;
-    if (split) {
+    if (split_long) {
+      rc = LaunchLong(ctx, static_cast<const uint8_t*>(base), off + pos, len + pos,
+                      init ? init + pos : nullptr, out + pos, n, mask, st);
+    } else if (split) {
       rc = LaunchClasses(ctx, static_cast<const uint8_t*>(base), off + pos, len + pos,
                          init ? init + pos : nullptr, out + pos, n, 0, mask, st);
     } else {
@@ -807,7 +875,8 @@ int hcrc_ctx_device(hcrc_ctx* ctx) { return ctx ? ctx->device : -1; }
 int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const uint32_t* lengths,
                const uint32_t* init_crcs, uint32_t* out_crcs, size_t count, int flags) {
   if (!ctx || (count && (!base || !offsets || !lengths || !out_crcs))) return HCRC_ERR_INVALID;
-  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL)) return HCRC_ERR_INVALID;
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG))
+    return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
   HCRC_DEVICE(ctx);
   if (flags & HCRC_DEVICE_PTRS) {
@@ -828,7 +897,8 @@ int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offset
                      const uint32_t* d_lengths, const uint32_t* d_init_crcs, uint32_t* d_out_crcs,
                      size_t count, int flags, void* stream) {
   if (!ctx || !(flags & HCRC_DEVICE_PTRS)) return HCRC_ERR_INVALID;
-  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL)) return HCRC_ERR_INVALID;
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG))
+    return HCRC_ERR_INVALID;
   if (count && (!d_base || !d_offsets || !d_lengths || !d_out_crcs)) return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
   HCRC_DEVICE(ctx);
