@@ -145,7 +145,10 @@ __global__ __launch_bounds__(256) void split_expand_kernel(
     const uint64_t i = base + lane;
     const bool live = i < count;
     const uint32_t n = live ? len[i] : 0u;
-    uint32_t m = (live && n >= thresh) ? (n + part - 1u) / part : (live ? 1u : 0u);
+    // (64-bit: a length near 4 GiB must not wrap)
+    uint32_t m = (live && n >= thresh)
+                     ? static_cast<uint32_t>((static_cast<uint64_t>(n) + part - 1u) / part)
+                     : (live ? 1u : 0u);
     // part slots for the long ones
     const uint32_t want = m > 1u ? m : 0u;
     const uint32_t incl = wave_scan(want, lane);
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(256) void split_combine_kernel(
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < nsplit; w += nw) {
     const uint32_t i = split_idx[w];
-    const uint32_t m = (len[i] + part - 1u) / part;
+    const uint32_t m = static_cast<uint32_t>((static_cast<uint64_t>(len[i]) + part - 1u) / part);
     const uint32_t* t = tmp + count + first[i];
     uint32_t acc = 0;
     if (lane < m) {
