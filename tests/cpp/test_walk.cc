@@ -110,7 +110,7 @@ struct Case {
   uint32_t Run() {
     const uint64_t end = s_abs + n + (verify ? 4u : 0u);
     for (uint64_t a = s_abs; a < end; ++a) pages.insert(a >> 12);
-    SpanD d{s_abs - sbase, n, init, 0u, 7u};
+    SpanD d{s_abs - sbase, n, init, 7u};
     WalkE wk;
     wk.start(sbase, d, verify);
     CheckFast(d, wk);
@@ -218,7 +218,7 @@ void Check(std::vector<uint8_t>& buf, uint64_t sbase, uint64_t s_abs, uint32_t n
     ++g_cases;
     if (got != want || c.bad_read) {
       if (getenv("WALK_VERBOSE")) {
-        SpanD d{s_abs - sbase, n, init, 0u, 7u};
+        SpanD d{s_abs - sbase, n, init, 7u};
         WalkE wk;
         wk.start(sbase, d, false);
         fprintf(stderr, "F geo %x nseg %u nc0 %u pg %u\n", wk.geo, wk.nseg, wk.geo >> 18, unsigned(s_abs & 4095));

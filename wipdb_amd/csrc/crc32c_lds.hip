@@ -365,7 +365,7 @@ struct DescSrc {
   uint64_t count;
   uint32_t extra;  // verify: +1 type byte
   __device__ __forceinline__ SpanD get(uint64_t s) const {
-    return SpanD{off[s], len[s] + extra, kInit ? init[s] : 0u, 0u, s};
+    return SpanD{off[s], len[s] + extra, kInit ? init[s] : 0u, static_cast<uint32_t>(s)};
   }
 };
 
@@ -376,7 +376,7 @@ struct StridedSrc {
   uint32_t length, init;
   uint64_t count;
   __device__ __forceinline__ SpanD get(uint64_t s) const {
-    return SpanD{s * stride, length, init, 0u, s};
+    return SpanD{s * stride, length, init, static_cast<uint32_t>(s)};
   }
 };
 
@@ -389,7 +389,7 @@ struct ListSrc {
   const uint32_t* id;
   uint64_t count;
   __device__ __forceinline__ SpanD get(uint64_t s) const {
-    return SpanD{off[s], len[s], init[s], 0u, id[s]};
+    return SpanD{off[s], len[s], init[s], id[s]};
   }
 };
 
@@ -864,12 +864,17 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
 // ---------------------------------------------------------------------------
 template <int G>
 struct GroupSpan {
-  uint64_t a0;       // offset of the span's first chunk
-  uint32_t nc;       // full chunks (<= 256 / G)
-  uint32_t h, o, e;  // head bytes, tail range
+  uint64_t a0;  // offset of the span's first chunk
+  // full chunks (<= 256 / G) | head bytes << 8 | tail range [o, e) << 12, 16 |
+  // valid << 24 -- packed: the G-span loop is short of SGPRs
+  uint32_t pk;
   uint32_t init;
   uint32_t id;
-  bool valid;
+  __device__ __forceinline__ uint32_t nc() const { return pk & 0xffu; }
+  __device__ __forceinline__ uint32_t h() const { return (pk >> 8) & 15u; }
+  __device__ __forceinline__ uint32_t o() const { return (pk >> 12) & 15u; }
+  __device__ __forceinline__ uint32_t e() const { return (pk >> 16) & 31u; }
+  __device__ __forceinline__ bool valid() const { return (pk >> 24) != 0u; }
 };
 
 template <int G, int OUT>
@@ -892,30 +897,26 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
   // descriptors of the next G units (SMEM, waited for at first use)
   struct Pref {
     SpanD d[G];
-    bool valid[G];
+    uint32_t nv;  // groups with a span (the first nv)
   };
   auto prefetch = [&](Pref& p) {
     const uint64_t s0 = grab_units<G>(l);
+    p.nv = s0 >= count ? 0u : static_cast<uint32_t>(count - s0 < G ? count - s0 : G);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      p.valid[g] = s0 + g < count;
-      if (p.valid[g]) p.d[g] = src.get(s0 + g);
-    }
+    for (int g = 0; g < G; ++g)
+      if (static_cast<uint32_t>(g) < p.nv) p.d[g] = src.get(s0 + g);
   };
   auto take = [&](const Pref& p, GS (&gs)[G]) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      gs[g].valid = p.valid[g];
-      gs[g].nc = gs[g].h = gs[g].o = gs[g].e = gs[g].init = gs[g].id = 0;
+      gs[g].pk = gs[g].init = gs[g].id = 0;
       gs[g].a0 = 0;
-      if (!p.valid[g]) continue;
+      if (static_cast<uint32_t>(g) >= p.nv) continue;
       const SpanD& d = p.d[g];
       const Geo geo(sbase + d.a, d.n);
       gs[g].a0 = d.a - geo.h;
-      gs[g].nc = geo.f;
-      gs[g].h = geo.h;
-      gs[g].o = geo.f == 0u ? geo.h : 0u;
-      gs[g].e = geo.t;
+      gs[g].pk = geo.f | (geo.h << 8) | ((geo.f == 0u ? geo.h : 0u) << 12) | (geo.t << 16) |
+                 (1u << 24);
       gs[g].init = d.init;
       gs[g].id = static_cast<uint32_t>(d.id);
     }
@@ -923,13 +924,13 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
   auto issue = [&](const GS (&gs)[G]) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      if (!gs[g].valid) continue;
-      if (gs[g].nc != 0u) {
-        if constexpr (G == 2) pp.issue<2>(sbase + gs[g].a0, 2u * g, CAP, gs[g].nc);
-        else pp.issue<1>(sbase + gs[g].a0, static_cast<uint32_t>(g), CAP, gs[g].nc);
+      if (!gs[g].valid()) continue;
+      if (gs[g].nc() != 0u) {
+        if constexpr (G == 2) pp.issue<2>(sbase + gs[g].a0, 2u * g, CAP, gs[g].nc());
+        else pp.issue<1>(sbase + gs[g].a0, static_cast<uint32_t>(g), CAP, gs[g].nc());
       }
-      pp.issue_end(sbase + gs[g].a0 + 16u * gs[g].nc, static_cast<uint32_t>(g),
-                   gs[g].e > gs[g].o, OUT == 1, gs[g].e);
+      pp.issue_end(sbase + gs[g].a0 + 16u * gs[g].nc(), static_cast<uint32_t>(g),
+                   gs[g].e() > gs[g].o(), OUT == 1, gs[g].e());
     }
   };
   // per-lane value of this lane's group: masked selects on per-group lane
@@ -951,7 +952,7 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
   Pref pf;
   GS cur[G], nxt[G];
   prefetch(pf);
-  if (!pf.valid[0]) return;
+  if (pf.nv == 0u) return;
   take(pf, cur);
   prefetch(pf);
   issue(cur);
@@ -969,7 +970,7 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
       next[g] = OUT == 1 ? pp.piece(kAuxNext + g) : u32x4{0, 0, 0, 0};
     }
     pp.release();
-    const bool more = pf.valid[0];
+    const bool more = pf.nv != 0u;
     if (more) {
       take(pf, nxt);
       issue(nxt);
@@ -980,9 +981,9 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
     bool fast = true;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      inj_g[g] = cur[g].valid ? head_register(l, cur[g].init, cur[g].h) : 0u;
-      nc_g[g] = cur[g].valid ? cur[g].nc : 0u;
-      h_g[g] = cur[g].h;
+      inj_g[g] = cur[g].valid() ? head_register(l, cur[g].init, cur[g].h()) : 0u;
+      nc_g[g] = cur[g].valid() ? cur[g].nc() : 0u;
+      h_g[g] = cur[g].h();
       fast = fast && nc_g[g] == CAP && h_g[g] == 0u;
     }
     const uint32_t inj = pick(inj_g);
@@ -1005,9 +1006,9 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
     uint32_t R[G], o_g[G], e_g[G], tw[4][G], nw[4][G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      R[g] = cur[g].nc == 0u ? ~cur[g].init : Rg[g];
-      o_g[g] = cur[g].o;
-      e_g[g] = cur[g].valid ? cur[g].e : 0u;
+      R[g] = cur[g].nc() == 0u ? ~cur[g].init : Rg[g];
+      o_g[g] = cur[g].o();
+      e_g[g] = cur[g].valid() ? cur[g].e() : 0u;
       tw[0][g] = tail[g].x;
       tw[1][g] = tail[g].y;
       tw[2][g] = tail[g].z;
@@ -1035,7 +1036,7 @@ __device__ __forceinline__ void run_g(const ListSrc& src, void* out, uint32_t fl
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       ids[g] = cur[g].id;
-      valid_l = valid_l || (gm[g] != 0u && cur[g].valid);
+      valid_l = valid_l || (gm[g] != 0u && cur[g].valid());
     }
     const uint32_t myid = pick(ids);
     if (gl == 0u && valid_l) {

@@ -18,8 +18,7 @@ struct SpanD {
   uint64_t a;      // offset of the first byte from the source base
   uint32_t n;      // bytes
   uint32_t init;   // Extend's init_crc
-  uint32_t link;   // (unused: keeps the layout of the list sources)
-  uint64_t id;     // output slot
+  uint32_t id;     // output slot (launches hold < 2^31 spans)
 };
 
 // Byte mask of word ww of chunk 0: its first h bytes are not the span's.
