@@ -224,9 +224,11 @@ __global__ __launch_bounds__(256) void split_combine_kernel(
     uint32_t kpart, uint32_t mask) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nsplit = counters[2];
+  const uint32_t w0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (w0 >= nsplit) return;  // (most waves of a batch with few long spans)
   const uint32_t k64 = powmod(kpart, 64);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < nsplit; w += nw) {
+  for (uint32_t w = w0; w < nsplit; w += nw) {
     const uint32_t i = split_idx[w];
     const uint32_t m = static_cast<uint32_t>((static_cast<uint64_t>(len[i]) + part - 1u) / part);
     const uint32_t* t = tmp + count + first[i];
