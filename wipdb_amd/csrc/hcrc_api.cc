@@ -15,10 +15,12 @@
 // different streams at the same time.  Every entry point restores the
 // caller's current HIP device before it returns.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -505,6 +507,10 @@ class CopyPool {
   }
   // fn(a, b) over [0, n) in parts, the caller running one of them
   void Run(size_t n, const std::function<void(size_t, size_t)>& fn) {
+    if (g_forked_child.load(std::memory_order_relaxed)) {  // no helpers after fork()
+      fn(0, n);
+      return;
+    }
     std::unique_lock<std::mutex> run(run_mu_, std::try_to_lock);
     if (!run.owns_lock() || workers_.empty()) {
       fn(0, n);
@@ -527,7 +533,10 @@ class CopyPool {
   }
 
  private:
+  static std::atomic<bool> g_forked_child;
   CopyPool() {
+    // a forked child inherits neither the helper threads nor consistent locks
+    pthread_atfork(nullptr, nullptr, [] { g_forked_child.store(true); });
     const unsigned hw = std::thread::hardware_concurrency();
     const unsigned nt = std::min(7u, hw > 1 ? hw - 1 : 0u);
     for (unsigned t = 0; t < nt; ++t) workers_.emplace_back([this, t] { Loop(t + 1); });
@@ -558,6 +567,7 @@ class CopyPool {
   size_t n_ = 0, per_ = 0, pending_ = 0;
   uint64_t gen_ = 0;
 };
+std::atomic<bool> CopyPool::g_forked_child{false};
 
 // Copy spans [lo, hi) into a slot's pinned buffer, keeping each span's
 // address mod 16 (so aligned blocks stay on the aligned fast path and the
