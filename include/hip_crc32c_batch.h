@@ -102,8 +102,13 @@ int hcrc_abi_version(void);
 int hcrc_device_count(int* count);
 const char* hcrc_strerror(int code);
 
-/* One context per device (idempotent per thread of use). */
+/* A context per call of hcrc_ctx_create (its own tables, streams, staging),
+ * released by hcrc_ctx_destroy.  hcrc_ctx_shared is idempotent per device
+ * (SURVEY 8b): every call returns the same process-wide context for that
+ * device, created on first use (the one the C++ ExtendBatch and
+ * hcrc_batch_multi use); it lives until the process ends unless destroyed. */
 int hcrc_ctx_create(int device, hcrc_ctx** out_ctx);
+int hcrc_ctx_shared(int device, hcrc_ctx** out_ctx);
 int hcrc_ctx_destroy(hcrc_ctx* ctx);
 /* The context's own HIP stream (hipStream_t as void*). */
 void* hcrc_ctx_stream(hcrc_ctx* ctx);

@@ -32,6 +32,7 @@ def test_abi_version_and_strerror():
 def test_invalid_arguments_are_rejected_without_device():
     lib = _lib.load()
     assert lib.hcrc_ctx_create(0, None) == _lib.HCRC_ERR_INVALID
+    assert lib.hcrc_ctx_shared(0, None) == _lib.HCRC_ERR_INVALID
     assert lib.hcrc_ctx_destroy(None) == _lib.HCRC_ERR_INVALID
     assert lib.hcrc_batch(None, None, None, None, None, None, 0, 0) == _lib.HCRC_ERR_INVALID
     assert lib.hcrc_batch_async(None, None, None, None, None, None, 0, 1, None) == _lib.HCRC_ERR_INVALID

@@ -334,6 +334,25 @@ def test_device_batch_split_long(engine, oracle):
     torch.cuda.synchronize()
 
 
+def test_ctx_shared_is_idempotent_per_device():
+    """hcrc_ctx_shared (ctx creation idempotent per device): every
+    call returns the same process-wide context, usable like any other."""
+    import ctypes
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.hcrc_ctx_shared(0, ctypes.byref(a)) == 0
+    assert lib.hcrc_ctx_shared(0, ctypes.byref(b)) == 0
+    assert a.value and a.value == b.value
+    assert lib.hcrc_ctx_shared(10_000, ctypes.byref(b)) == _lib.HCRC_ERR_NO_DEVICE
+    data = np.frombuffer(b"123456789", np.uint8).copy()
+    off, ln = np.zeros(1, np.uint64), np.array([9], np.uint32)
+    out = np.zeros(1, np.uint32)
+    assert lib.hcrc_batch(a, data.ctypes.data, off.ctypes.data, ln.ctypes.data, None,
+                          out.ctypes.data, 1, 0) == 0
+    assert int(out[0]) == 0xE3069283  # CRC-32C check value
+
+
 def test_check_spans_bounds(engine):
     """hcrc_check_spans: the count and lowest index of spans that leave the
     base buffer, overflow-safe, for CRC (extra 0) and verify (extra 5)

@@ -44,6 +44,7 @@ _PROTOS = {
     "hcrc_device_count": (_c.c_int, [_c.POINTER(_c.c_int)]),
     "hcrc_strerror": (_c.c_char_p, [_c.c_int]),
     "hcrc_ctx_create": (_c.c_int, [_c.c_int, _c.POINTER(_vp)]),
+    "hcrc_ctx_shared": (_c.c_int, [_c.c_int, _c.POINTER(_vp)]),
     "hcrc_ctx_destroy": (_c.c_int, [_vp]),
     "hcrc_ctx_stream": (_vp, [_vp]),
     "hcrc_ctx_device": (_c.c_int, [_vp]),

@@ -78,9 +78,7 @@ std::atomic<uint64_t> g_gpu_batches{0}, g_cpu_batches{0};
 std::atomic<int> g_last_error{0};
 std::atomic<uint32_t> g_round_robin{0};
 std::mutex g_mu;
-hcrc_ctx* g_ctx[64] = {nullptr};
-int g_ctx_rc[64] = {0};
-bool g_ctx_tried[64] = {false};
+int g_ctx_rc[64] = {0};  // a device's first failure, kept
 
 // WIPDB_CRC_* (include/wipdb/crc32c.h), read once.
 struct EnvConfig {
@@ -116,15 +114,21 @@ const EnvConfig& Env() {
   return cfg;
 }
 
+// The process-wide context of a device (hcrc_ctx_shared, looked up per call:
+// a caller may have destroyed it), shared with hcrc_batch_multi; a device
+// that failed once is not retried.
 int CtxFor(int device, hcrc_ctx** out) {
   if (device < 0 || device >= 64) return HCRC_ERR_NO_DEVICE;
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_ctx_tried[device]) {
-    g_ctx_tried[device] = true;
-    g_ctx_rc[device] = hcrc_ctx_create(device, &g_ctx[device]);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ctx_rc[device] != HCRC_OK) return g_ctx_rc[device];
   }
-  *out = g_ctx[device];
-  return g_ctx_rc[device];
+  const int rc = hcrc_ctx_shared(device, out);
+  if (rc != HCRC_OK) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_ctx_rc[device] = rc;
+  }
+  return rc;
 }
 
 int GpuBatch(const char* base, const uint64_t* offsets, const uint32_t* lengths,

@@ -808,6 +808,12 @@ const char* hcrc_strerror(int code) {
   }
 }
 
+int hcrc_ctx_shared(int device, hcrc_ctx** out_ctx) {
+  if (!out_ctx) return HCRC_ERR_INVALID;
+  *out_ctx = nullptr;
+  return SharedCtx(device, out_ctx);
+}
+
 int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
   if (!out_ctx) return HCRC_ERR_INVALID;
   *out_ctx = nullptr;
