@@ -25,4 +25,4 @@ for i, sh in enumerate(shapes):
     cs = sorted(by[grp[0]])
     vals = {c: sum(by[g].get(c, 0) for g in grp) / len(grp) / n for c in cs}
     print(f"{sh['shape'][:34]:34s} {sh['ms']:.4f} ms " +
-          " ".join(f"{c.replace('SQ_INSTS_', '').replace('SQ_', '')}={v:.1f}" for c, v in vals.items()))
+          " ".join(f"{c.replace('SQ_INSTS_', '').replace('SQ_', '')}={v:.4g}" for c, v in vals.items()))
