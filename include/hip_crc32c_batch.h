@@ -106,7 +106,9 @@ const char* hcrc_strerror(int code);
  * released by hcrc_ctx_destroy.  hcrc_ctx_shared is idempotent per device
  * (SURVEY 8b): every call returns the same process-wide context for that
  * device, created on first use (the one the C++ ExtendBatch and
- * hcrc_batch_multi use); it lives until the process ends unless destroyed. */
+ * hcrc_batch_multi use); it lives until the process ends: hcrc_ctx_destroy
+ * refuses it (HCRC_ERR_INVALID), since other threads may hold it at any
+ * moment. */
 int hcrc_ctx_create(int device, hcrc_ctx** out_ctx);
 int hcrc_ctx_shared(int device, hcrc_ctx** out_ctx);
 int hcrc_ctx_destroy(hcrc_ctx* ctx);
@@ -216,6 +218,12 @@ int hcrc_fill_splitmix64_async(hcrc_ctx* ctx, void* d_dst, uint64_t nbytes,
 /* Host CPU path (from-scratch SSE4.2+PCLMUL 3-stream, or portable
  * slicing-by-8); the function kv::crc32c::Extend is built on. */
 uint32_t hcrc_cpu_extend(uint32_t init_crc, const void* data, size_t n);
+/* The portable slicing-by-8 path alone, whatever the CPU supports (the
+ * reference's ExtendImpl<Slow_CRC32>, kv/src/util/crc32c.cc:325-339,
+ * 355-397).  WIPDB_CRC_PORTABLE=1 in the environment makes hcrc_cpu_extend,
+ * hcrc_cpu_batch and the C++ surface use it too (and
+ * hcrc_cpu_is_accelerated return 0), as on a host without SSE4.2. */
+uint32_t hcrc_cpu_extend_portable(uint32_t init_crc, const void* data, size_t n);
 int hcrc_cpu_batch(const void* base, const uint64_t* offsets,
                    const uint32_t* lengths, const uint32_t* init_crcs,
                    uint32_t* out_crcs, size_t count, int flags, int threads);

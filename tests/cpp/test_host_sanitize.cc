@@ -66,12 +66,15 @@ void CpuCrc() {
   // exact-size heap buffers so any over-read is an ASan report
   const uint8_t kat[] = "123456789";
   CHECK(hcrc_cpu_extend(0, kat, 9) == 0xE3069283u);
+  CHECK(hcrc_cpu_extend_portable(0, kat, 9) == 0xE3069283u);
   for (size_t n = 0; n < 2100; n += (n < 600 ? 1 : 37)) {
     for (size_t a = 0; a < 16; a += (n < 300 ? 1 : 5)) {
       uint8_t* buf = static_cast<uint8_t*>(malloc(a + n + 1));
       for (size_t i = 0; i < a + n; ++i) buf[i] = static_cast<uint8_t>(Rnd());
       const uint32_t init = static_cast<uint32_t>(Rnd());
       CHECK(hcrc_cpu_extend(init, buf + a, n) == Sarwate(init, buf + a, n));
+      // the portable slicing-by-8 fallback on the same exact-size buffer
+      CHECK(hcrc_cpu_extend_portable(init, buf + a, n) == Sarwate(init, buf + a, n));
       free(buf);
     }
   }
@@ -79,6 +82,7 @@ void CpuCrc() {
     std::vector<uint8_t> v(n);
     for (auto& b : v) b = static_cast<uint8_t>(Rnd());
     CHECK(hcrc_cpu_extend(7, v.data(), n) == Sarwate(7, v.data(), n));
+    CHECK(hcrc_cpu_extend_portable(7, v.data(), n) == Sarwate(7, v.data(), n));
   }
   // batch, 4 threads, inits and masks
   std::vector<uint8_t> base(1 << 20);

@@ -72,6 +72,7 @@ _PROTOS = {
     "hcrc_fill_splitmix64_async": (
         _c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint64, _c.c_uint64, _vp]),
     "hcrc_cpu_extend": (_c.c_uint32, [_c.c_uint32, _vp, _sz]),
+    "hcrc_cpu_extend_portable": (_c.c_uint32, [_c.c_uint32, _vp, _sz]),
     "hcrc_cpu_batch": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _c.c_int, _c.c_int]),
     "hcrc_cpu_is_accelerated": (_c.c_int, []),
     "hcrc_mask": (_c.c_uint32, [_c.c_uint32]),

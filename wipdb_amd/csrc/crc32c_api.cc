@@ -24,6 +24,7 @@
 namespace wipdb {
 namespace cpu {
 uint32_t Extend(uint32_t init_crc, const void* data, size_t n);
+uint32_t ExtendPortable(uint32_t init_crc, const void* data, size_t n);
 bool IsAccelerated();
 void Batch(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
            const uint32_t* inits, uint32_t* out, size_t count, bool mask,
@@ -192,6 +193,10 @@ extern "C" {
 
 uint32_t hcrc_cpu_extend(uint32_t init_crc, const void* data, size_t n) {
   return wipdb::cpu::Extend(init_crc, data, n);
+}
+
+uint32_t hcrc_cpu_extend_portable(uint32_t init_crc, const void* data, size_t n) {
+  return wipdb::cpu::ExtendPortable(init_crc, data, n);
 }
 
 int hcrc_cpu_batch(const void* base, const uint64_t* offsets,

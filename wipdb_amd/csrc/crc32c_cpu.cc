@@ -17,6 +17,7 @@
 //    crc32c_3way/CombineCRC (crc32c.cc:640-1198), own derivation: the fold
 //    constants are computed at start-up from gf2::XPowBits, not tabulated.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -135,13 +136,25 @@ __attribute__((target("sse4.2,pclmul"))) uint32_t FeedSse42(uint32_t r,
 }
 #endif
 
+// WIPDB_CRC_PORTABLE=1 in the environment forces the portable path on a
+// host that has SSE4.2 + PCLMUL -- the reference's Choose_Extend falling to
+// ExtendImpl<Slow_CRC32> (kv/src/util/crc32c.cc:1202-1222), made reachable
+// so the portable path is exercised (tests/test_cpu_path.py).
+bool ForcePortable() {
+  static const bool force = [] {
+    const char* e = getenv("WIPDB_CRC_PORTABLE");
+    return e && *e && strcmp(e, "0") != 0;
+  }();
+  return force;
+}
+
 }  // namespace
 
 // Raw register feed (no pre/post inversion).
 uint32_t Feed(uint32_t reg, const void* data, size_t n) {
   const uint8_t* p = static_cast<const uint8_t*>(data);
 #ifdef WIPDB_X86
-  if (HaveSse42Clmul()) return FeedSse42(reg, p, n);
+  if (HaveSse42Clmul() && !ForcePortable()) return FeedSse42(reg, p, n);
 #endif
   return FeedPortable(reg, p, n);
 }
@@ -156,7 +169,7 @@ uint32_t ExtendPortable(uint32_t init_crc, const void* data, size_t n) {
 
 bool IsAccelerated() {
 #ifdef WIPDB_X86
-  return HaveSse42Clmul();
+  return HaveSse42Clmul() && !ForcePortable();
 #else
   return false;
 #endif

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -286,6 +287,19 @@ class LaneLease {
     }
   }
   ~LaneLease() {
+    // An error return mid-batch can leave a slot with a piece in flight and
+    // the caller's output pointer recorded: wait for the stream and forget
+    // those pointers, so the next lessee's Drain() never writes into a
+    // buffer the failed call's caller (or BatchHostLong's temporary) owned.
+    bool pending = false;
+    for (const Slot& s : lane_->slots) pending = pending || s.user_out != nullptr;
+    if (pending) {
+      if (lane_->stream) (void)hipStreamSynchronize(lane_->stream);
+      for (Slot& s : lane_->slots) {
+        s.user_out = nullptr;
+        s.n_out = 0;
+      }
+    }
     {
       std::lock_guard<std::mutex> lk(ctx_->lanes_mu);
       ctx_->free_lanes.push_back(lane_);
@@ -569,6 +583,20 @@ class CopyPool {
 };
 std::atomic<bool> CopyPool::g_forked_child{false};
 
+// Test hook (fault injection, tests/test_gpu_parity.py): with
+// WIPDB_HCRC_FAIL_PIECE=k in the environment, the first host batch that
+// reaches its k-th piece fails there with HCRC_ERR_LAUNCH while the previous
+// piece is still in flight -- the error path LaneLease must clean up.  Fires
+// once per process.
+bool InjectedPieceFault(size_t piece) {
+  static const long at = [] {
+    const char* e = getenv("WIPDB_HCRC_FAIL_PIECE");
+    return e && *e ? atol(e) : -1L;
+  }();
+  static std::atomic<bool> fired{false};
+  return at >= 0 && piece == static_cast<size_t>(at) && !fired.exchange(true);
+}
+
 // Copy spans [lo, hi) into a slot's pinned buffer, keeping each span's
 // address mod 16 (so aligned blocks stay on the aligned fast path and the
 // size classes are the caller's).
@@ -600,12 +628,13 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
                   const uint8_t* host_base, const uint64_t* offsets, const uint32_t* lengths,
                   const uint32_t* inits, uint32_t* out, size_t count, int flags) {
   const hipStream_t st = lane->stream;
-  size_t i = 0;
+  size_t i = 0, piece = 0;
   int k = 0;
   while (i < count) {
     Slot& s = lane->slots[k];
     int rc = s.Drain();
     if (rc) return rc;
+    if (InjectedPieceFault(piece++)) return HCRC_ERR_LAUNCH;
     const size_t n = std::min(count - i, kStageSpans);
     memcpy(s.h_off, offsets + i, n * 8);
     memcpy(s.h_len, lengths + i, n * 4);
@@ -638,12 +667,13 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
   if (const uint8_t* dev = MappedSpans(base, offsets, lengths, count))
     return BatchZeroCopy(ctx, lane, dev, base, offsets, lengths, inits, out, count, flags);
   const hipStream_t st = lane->stream;
-  size_t i = 0;
+  size_t i = 0, piece = 0;
   int k = 0;
   while (i < count) {
     Slot& s = lane->slots[k];
     rc = s.Drain();
     if (rc) return rc;
+    if (InjectedPieceFault(piece++)) return HCRC_ERR_LAUNCH;
     // piece = spans [i, j) fitting the slot (a single larger span grows it)
     size_t bytes = 0, j = i;
     while (j < count && j - i < kStageSpans) {
@@ -863,10 +893,11 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
 int hcrc_ctx_destroy(hcrc_ctx* ctx) {
   if (!ctx) return HCRC_ERR_INVALID;
   {
+    // a shared context (hcrc_ctx_shared) lives until the process ends: other
+    // threads (ExtendBatch, hcrc_batch_multi) may hold it at any moment
     std::lock_guard<std::mutex> lk(g_ctx_mu);
-    auto& m = SharedCtxs();
-    auto it = m.find(ctx->device);
-    if (it != m.end() && it->second == ctx) m.erase(it);
+    for (const auto& kv : SharedCtxs())
+      if (kv.second == ctx) return HCRC_ERR_INVALID;
   }
   DeviceGuard dg(ctx->device);
   for (auto& lane : ctx->lanes) {
@@ -993,8 +1024,9 @@ int hcrc_check_spans_async(hcrc_ctx* ctx, uint64_t base_bytes, const uint64_t* d
   if (!ctx || !d_result || (count && (!d_offsets || !d_lengths))) return HCRC_ERR_INVALID;
   HCRC_DEVICE(ctx);
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  const uint64_t init[2] = {0, ~uint64_t(0)};
-  HCRC_CHECK(hipMemcpyAsync(d_result, init, sizeof(init), hipMemcpyHostToDevice, st));
+  // result words {0, ~0}: stream-ordered memsets, no host source in flight
+  HCRC_CHECK(hipMemsetAsync(d_result, 0, 8, st));
+  HCRC_CHECK(hipMemsetAsync(d_result + 1, 0xff, 8, st));
   if (count == 0) return HCRC_OK;
   const int grid =
       static_cast<int>(std::min<uint64_t>((count + 255) / 256, uint64_t(ctx->num_cu) * 8));
