@@ -1,0 +1,244 @@
+// tests/cpp/test_lp_emu.cc -- the lane-packed spans / verify / strided
+// kernels (wipdb_amd/csrc/crc32c_lds.hip, their own source) run on the host
+// under the SIMT emulation of tests/cpp/lk_emu.h, against a byte-serial
+// CRC32C: every span shape (short spans packed many per iteration, table
+// blocks as a segment + back piece, long spans shared through the
+// workgroup's queue, empty spans, inits, masked output), ReadBlock's verify
+// with good and corrupted trailers, and every DMA source inside the test's
+// buffer.  Catches control-flow and indexing errors of the kernel loop (the
+// desk, the ring, the queue, the batch packing) before a GPU run.
+// Build: clang++ -std=c++17 -O1 -pthread -I wipdb_amd/csrc -I tests/cpp.
+// Usage: test_lp_emu [case ...]; exit 0 = pass.
+#define WIPDB_LK_EMU 1
+#include "crc32c_lds.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <string>
+#include <vector>
+
+using namespace wipdb::lk;
+
+namespace {
+
+wipdb::gf2::Tables T;
+std::vector<uint32_t> g_image(kImageBytes / 4);
+
+uint32_t Extend(uint32_t init, const uint8_t* p, size_t n) {
+  uint32_t r = ~init;
+  for (size_t i = 0; i < n; ++i) r = T.t[0][(r ^ p[i]) & 0xffu] ^ (r >> 8);
+  return ~r;
+}
+
+int g_fail = 0;
+
+// DMA sources must lie in the pages of the buffer (the kernel's guarantee:
+// nothing outside the pages that hold bytes of a span is read)
+void SetRange(const std::vector<uint8_t>& buf) {
+  const uint64_t lo = reinterpret_cast<uint64_t>(buf.data());
+  emu::g_src_lo = lo & ~uint64_t(4095);
+  emu::g_src_hi = (lo + buf.size() + 4095) & ~uint64_t(4095);
+}
+
+uint32_t Grid(size_t count, uint32_t cus) {
+  const size_t need = (count + 15) / 16;
+  return static_cast<uint32_t>(need < cus ? (need ? need : 1) : cus);
+}
+
+void Report(const char* name, const std::vector<uint32_t>& got, const std::vector<uint32_t>& want,
+            const std::vector<uint64_t>& offs, const std::vector<uint32_t>& lens) {
+  size_t bad = 0;
+  for (size_t i = 0; i < want.size(); ++i) {
+    if (got[i] != want[i]) {
+      if (bad < 6)
+        fprintf(stderr, "  %s: span %zu off %llu len %u: got %08x want %08x\n", name, i,
+                (unsigned long long)offs[i], lens[i], got[i], want[i]);
+      ++bad;
+    }
+  }
+  const uint64_t bs = emu::g_bad_src.exchange(0);
+  if (bs) fprintf(stderr, "  %s: DMA source %#llx outside the buffer\n", name, (unsigned long long)(bs & ~1ull));
+  printf("%-34s %6zu spans  %s (%zu bad)\n", name, want.size(), bad || bs ? "FAIL" : "ok", bad);
+  if (bad || bs) ++g_fail;
+}
+
+// CRC batch through crc32c_lds_spans_kernel
+void RunSpans(const char* name, std::vector<uint8_t>& buf, const std::vector<uint64_t>& offs,
+              const std::vector<uint32_t>& lens, const std::vector<uint32_t>* inits, bool mask,
+              uint32_t cus) {
+  const size_t n = offs.size();
+  std::vector<uint32_t> want(n), got(n, 0x5A5A5A5Au);
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t c = Extend(inits ? (*inits)[i] : 0u, buf.data() + offs[i], lens[i]);
+    want[i] = mask ? wipdb::gf2::Mask(c) : c;
+  }
+  SetRange(buf);
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
+  emu::launch(Grid(n, cus), [&] {
+    if (inits)
+      crc32c_lds_spans_kernel<1>(buf.data(), offs.data(), lens.data(), inits->data(), got.data(), n,
+                                 mask ? kFlagMask : 0u, img);
+    else
+      crc32c_lds_spans_kernel<0>(buf.data(), offs.data(), lens.data(), nullptr, got.data(), n,
+                                 mask ? kFlagMask : 0u, img);
+  });
+  Report(name, got, want, offs, lens);
+}
+
+// ReadBlock verify: spans of n bytes (contents + type) followed by a masked
+// trailer; every 7th block corrupted
+void RunVerify(const char* name, std::vector<uint8_t>& buf, const std::vector<uint64_t>& offs,
+               const std::vector<uint32_t>& lens, uint32_t cus) {
+  const size_t n = offs.size();
+  std::vector<uint32_t> want(n), hl(n);
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t m = wipdb::gf2::Mask(Extend(0u, buf.data() + offs[i], lens[i]));
+    memcpy(buf.data() + offs[i] + lens[i], &m, 4);
+    want[i] = 1;
+    if (i % 7 == 3) {
+      buf[offs[i] + (i % 5 == 0 ? lens[i] + 2 : lens[i] / 2)] ^= 0x40;  // data or trailer
+      want[i] = 0;
+    }
+    hl[i] = lens[i] - 1;  // handle size (the type byte is the +1)
+  }
+  std::vector<uint8_t> st(n, 0x5A);
+  SetRange(buf);
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
+  emu::launch(Grid(n, cus), [&] {
+    crc32c_lds_verify_kernel(buf.data(), offs.data(), hl.data(), st.data(), n, img);
+  });
+  std::vector<uint32_t> got(st.begin(), st.end());
+  Report(name, got, want, offs, lens);
+  for (size_t i = 0; i < n; ++i)  // undo the corruption
+    if (i % 7 == 3) buf[offs[i] + (i % 5 == 0 ? lens[i] + 2 : lens[i] / 2)] ^= 0x40;
+}
+
+void RunStrided(const char* name, std::vector<uint8_t>& buf, uint64_t stride, uint32_t len,
+                uint32_t init, size_t n, uint32_t cus) {
+  std::vector<uint64_t> offs(n);
+  std::vector<uint32_t> lens(n, len), want(n), got(n, 0x5A5A5A5Au);
+  for (size_t i = 0; i < n; ++i) {
+    offs[i] = i * stride;
+    want[i] = Extend(init, buf.data() + offs[i], len);
+  }
+  SetRange(buf);
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
+  emu::launch(Grid(n, cus), [&] {
+    crc32c_lds_strided_kernel(buf.data(), stride, len, init, got.data(), n, 0u, img);
+  });
+  Report(name, got, want, offs, lens);
+}
+
+std::vector<uint64_t> Packed(const std::vector<uint32_t>& lens, uint64_t start, uint32_t gap) {
+  std::vector<uint64_t> o(lens.size());
+  uint64_t cur = start;
+  for (size_t i = 0; i < lens.size(); ++i) {
+    o[i] = cur;
+    cur += lens[i] + gap;
+  }
+  return o;
+}
+
+bool Want(int argc, char** argv, const char* name) {
+  if (argc < 2) return true;
+  for (int i = 1; i < argc; ++i)
+    if (strstr(name, argv[i])) return true;
+  return false;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  wipdb::gf2::BuildTables(&T);
+  BuildLdsImage(g_image.data());
+  std::mt19937_64 rng(7);
+  std::vector<uint8_t> buf(24u << 20);
+  for (auto& b : buf) b = static_cast<uint8_t>(rng());
+  auto lens_of = [&](size_t n, uint32_t lo, uint32_t hi) {
+    std::vector<uint32_t> v(n);
+    for (auto& x : v) x = lo + static_cast<uint32_t>(rng() % (hi - lo + 1));
+    return v;
+  };
+  auto inits_of = [&](size_t n) {
+    std::vector<uint32_t> v(n);
+    for (size_t i = 0; i < n; ++i) v[i] = i % 3 ? static_cast<uint32_t>(rng()) : 0u;
+    return v;
+  };
+  if (Want(argc, argv, "one short")) RunSpans("one short", buf, {64}, {100}, nullptr, false, 1);
+  if (Want(argc, argv, "one 4096")) RunSpans("one 4096", buf, {4096}, {4096}, nullptr, false, 1);
+  if (Want(argc, argv, "one 5000")) RunSpans("one 5000", buf, {4099}, {5000}, nullptr, false, 1);
+  if (Want(argc, argv, "17 short")) {
+    std::vector<uint64_t> o;
+    for (int i = 0; i < 17; ++i) o.push_back(128u * i);
+    RunSpans("17 short", buf, o, std::vector<uint32_t>(17, 100), nullptr, false, 1);
+  }
+  if (Want(argc, argv, "tiny 0..40")) {
+    std::vector<uint32_t> l;
+    std::vector<uint64_t> o;
+    for (uint32_t n = 0; n <= 40; ++n)
+      for (uint32_t a = 0; a < 8; ++a) {
+        l.push_back(n);
+        o.push_back(4096u * 3 - 20 + a + 64u * n);
+      }
+    auto in = inits_of(l.size());
+    RunSpans("tiny 0..40 (inits)", buf, o, l, &in, false, 2);
+  }
+  if (Want(argc, argv, "short 0..300")) {
+    auto l = lens_of(3000, 0, 300);
+    auto in = inits_of(l.size());
+    RunSpans("short 0..300 packed (inits)", buf, Packed(l, 5, 3), l, &in, false, 3);
+  }
+  if (Want(argc, argv, "512 bucket")) {
+    auto l = lens_of(3000, 512, 576);
+    RunSpans("512 bucket packed", buf, Packed(l, 3, 5), l, nullptr, true, 4);
+  }
+  if (Want(argc, argv, "aligned 4 KiB")) {
+    std::vector<uint64_t> o;
+    for (int i = 0; i < 2000; ++i) o.push_back(4096u * i);
+    RunSpans("aligned 4 KiB", buf, o, std::vector<uint32_t>(2000, 4096), nullptr, false, 3);
+  }
+  if (Want(argc, argv, "table blocks")) {
+    auto l = lens_of(2000, 4097, 4225);
+    RunSpans("table blocks", buf, Packed(l, 0, 4), l, nullptr, true, 3);
+  }
+  if (Want(argc, argv, "near 4 KiB")) {
+    auto l = lens_of(2000, 3960, 4240);
+    auto in = inits_of(l.size());
+    RunSpans("near 4 KiB (inits)", buf, Packed(l, 1, 7), l, &in, false, 3);
+  }
+  if (Want(argc, argv, "long")) {
+    auto l = lens_of(300, 8000, 70000);
+    RunSpans("long 8..70 KiB", buf, Packed(l, 2, 5), l, nullptr, false, 2);
+  }
+  if (Want(argc, argv, "zipf mix")) {
+    const uint32_t B[] = {512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+    std::vector<uint32_t> l;
+    for (int i = 0; i < 1500; ++i) {
+      const double u = (rng() >> 11) * (1.0 / 9007199254740992.0);
+      int k = 0;
+      double c = 0, z = 0;
+      for (int j = 0; j < 8; ++j) z += 1.0 / (j + 1);
+      for (; k < 7; ++k) {
+        c += 1.0 / (k + 1) / z;
+        if (u < c) break;
+      }
+      l.push_back(B[k] + static_cast<uint32_t>(rng() % (B[k] / 8 + 1)));
+    }
+    RunSpans("zipf mix", buf, Packed(l, 3, 5), l, nullptr, false, 4);
+  }
+  if (Want(argc, argv, "verify")) {
+    auto l = lens_of(1500, 1, 5000);
+    RunVerify("verify mixed", buf, Packed(l, 9, 4), l, 3);
+    auto l2 = lens_of(1000, 4096, 4225);
+    RunVerify("verify table blocks", buf, Packed(l2, 0, 4), l2, 3);
+  }
+  if (Want(argc, argv, "strided")) {
+    RunStrided("strided 4096", buf, 4096, 4096, 0, 1500, 3);
+    RunStrided("strided 700 / 513 (init)", buf, 700, 513, 0x12345678u, 1500, 2);
+  }
+  printf("%s: %d failing cases\n", g_fail ? "FAIL" : "PASS", g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -66,7 +66,22 @@ WIPDB_LK_HD constexpr uint32_t MiscAddr(uint32_t i) {
 constexpr uint32_t kMiscInvTop = 0;    // 256 words: inv_top[v] (gf2::Tables)
 constexpr uint32_t kMiscHead0 = 256;   // 16 words: ~0 * x^(-8h)
 constexpr uint32_t kMiscUnit = 272;    // the workgroup's unit counter
+constexpr uint32_t kMiscQHead = 273;   // the long-span queue's head / tail (run_lp)
+constexpr uint32_t kMiscQTail = 274;
 constexpr uint32_t kMiscBytes = 1024 * 4;
+
+// run_lp (the lane-packed spans / strided / verify kernels):
+//   * the workgroup's long-span queue: 256 records of 16 bytes in the a = 0
+//     column of the main rows (bytes 128..143 of row k; the list kernels
+//     keep their aux pieces there instead): {a_lo, a_hi, n, span + 1}, a
+//     last word of 0 = a free slot;
+//   * wave w's aux chunk of a segment tail: the c = 0 column of level-2 row
+//     128 + w (misc words 512.. are unused).
+constexpr uint32_t kQSlots = 256;
+WIPDB_LK_HD constexpr uint32_t QRecAddr(uint32_t k) {
+  return kLdsMain + (k & (kQSlots - 1u)) * 256u + 128u;
+}
+WIPDB_LK_HD constexpr uint32_t SegAuxAddr(uint32_t w) { return kLdsL2 + (128u + w) * 128u; }
 
 // Flags of a launch (the HCRC_MASK_OUTPUT value is shared with the C-ABI).
 constexpr uint32_t kFlagMask = 0x2;

@@ -1,0 +1,192 @@
+// crc32c_prim.h -- the gfx950 hardware primitives the LDS-staged CRC32C
+// kernels are written in (crc32c_dev.h, crc32c_lds.hip): LDS access and
+// atomics, cross-lane operations (DPP, ballot, readlane, ds_bpermute),
+// global_load_lds DMA and the hand-counted waits.  tests/cpp/lk_emu.h
+// defines the same functions on the host (one thread per lane), so the
+// kernels' own source runs there for the CPU test suite (tests/cpp/
+// test_lp_emu.cc); nothing else differs between the two builds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wipdb {
+namespace lk {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const uint32_t l_u32;
+typedef __attribute__((address_space(3))) uint32_t l_u32w;
+typedef __attribute__((address_space(3))) const u32x4 l_u32x4;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+
+// ---- LDS (byte addresses) ----
+__device__ __forceinline__ uint32_t lds_ld(uint32_t a) {
+  return *reinterpret_cast<l_u32*>(static_cast<uintptr_t>(a));
+}
+__device__ __forceinline__ u32x4 lds_ld4(uint32_t a) {
+  return *reinterpret_cast<l_u32x4*>(static_cast<uintptr_t>(a));
+}
+__device__ __forceinline__ l_u32w* lds_p(uint32_t a) {
+  return reinterpret_cast<l_u32w*>(static_cast<uintptr_t>(a));
+}
+__device__ __forceinline__ uint32_t lds_add(uint32_t a, uint32_t v) {
+  return __atomic_fetch_add(lds_p(a), v, __ATOMIC_RELAXED);
+}
+__device__ __forceinline__ uint32_t lds_cas(uint32_t a, uint32_t cmp, uint32_t v) {
+  uint32_t c = cmp;
+  __atomic_compare_exchange_n(lds_p(a), &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+  return c;  // the old value
+}
+// uncached (another wave may write it)
+__device__ __forceinline__ uint32_t lds_ld_sync(uint32_t a) {
+  return __atomic_load_n(lds_p(a), __ATOMIC_RELAXED);
+}
+__device__ __forceinline__ void lds_st_sync(uint32_t a, uint32_t v) {
+  __atomic_store_n(lds_p(a), v, __ATOMIC_RELAXED);
+}
+// every LDS access of this wave has completed (and none moves across)
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void compiler_barrier() { asm volatile("" ::: "memory"); }
+
+// ---- lanes ----
+__device__ __forceinline__ uint32_t lane_tid() { return threadIdx.x; }
+__device__ __forceinline__ uint32_t group_id() { return blockIdx.x; }
+__device__ __forceinline__ uint32_t group_count() { return gridDim.x; }
+__device__ __forceinline__ void wg_sync() { __syncthreads(); }
+__device__ __forceinline__ void lk_sleep() { __builtin_amdgcn_s_sleep(1); }
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t vperm(uint32_t a, uint32_t b, uint32_t sel) {
+  return __builtin_amdgcn_perm(a, b, sel);
+}
+// DPP move (lanes without a source read 0)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, 0xF, 0xF, true));
+}
+// uniform value of the wave (all lanes active)
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return (static_cast<uint64_t>(uni(static_cast<uint32_t>(v >> 32))) << 32) |
+         uni(static_cast<uint32_t>(v));
+}
+// a value the active lanes agree on, said to be uniform (any exec mask)
+__device__ __forceinline__ uint32_t uni_act(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni_act64(uint64_t v) {
+  return (static_cast<uint64_t>(uni_act(static_cast<uint32_t>(v >> 32))) << 32) |
+         uni_act(static_cast<uint32_t>(v));
+}
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t k) {
+  return __builtin_amdgcn_readlane(v, k);
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t mbcnt_lo(uint32_t m, uint32_t acc) {
+  return __builtin_amdgcn_mbcnt_lo(m, acc);
+}
+__device__ __forceinline__ uint32_t mbcnt_hi(uint32_t m, uint32_t acc) {
+  return __builtin_amdgcn_mbcnt_hi(m, acc);
+}
+__device__ __forceinline__ uint32_t bperm_raw(uint32_t v, uint32_t lane) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(lane << 2),
+                                                            static_cast<int>(v)));
+}
+
+// ---------------------------------------------------------------------------
+// DMA.  The LDS destination of global_load_lds is M0 + 16 * lane (lane-
+// linear); the source address is per lane (SGPR base + VGPR offset).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void dma4(uint64_t base, uint32_t slot, uint32_t o0, uint32_t o1,
+                                     uint32_t o2, uint32_t o3) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %6 nt\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %6 nt\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %3, %6 nt\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %4, %6 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(o0), "v"(o1), "v"(o2), "v"(o3), "s"(slot), "s"(base)
+      : "memory", "scc");
+}
+
+__device__ __forceinline__ void dma1(uint64_t base, uint32_t dst, uint32_t off) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(dst), "s"(base)
+      : "memory");
+}
+
+__device__ __forceinline__ void dma2(uint64_t base, uint32_t slot, uint32_t o0, uint32_t o1) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %4 nt\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %4 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(o0), "v"(o1), "s"(slot), "s"(base)
+      : "memory", "scc");
+}
+
+__device__ __forceinline__ void dma1nt(uint64_t base, uint32_t dst, uint32_t off) {
+  uint32_t keep;
+  // (callers' values are uniform; say so, so they stay in SGPRs under a lane branch)
+  dst = uni_act(dst);
+  base = uni_act64(base);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(dst), "s"(base)
+      : "memory");
+}
+
+// One DMA with per-lane 64-bit source addresses (the lanes of one
+// instruction may serve different spans).
+__device__ __forceinline__ void dma1v(uint64_t addr, uint32_t dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(addr), "s"(dst)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+}
+
+
+}  // namespace lk
+}  // namespace wipdb

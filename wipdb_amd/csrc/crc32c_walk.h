@@ -9,22 +9,10 @@
 #include <stdint.h>
 
 #include "crc32c_lds.h"
+#include "crc32c_plan.h"
 
 namespace wipdb {
 namespace lk {
-
-// A span as a source hands it out (all values uniform).
-struct SpanD {
-  uint64_t a;      // offset of the first byte from the source base
-  uint32_t n;      // bytes
-  uint32_t init;   // Extend's init_crc
-  uint32_t id;     // output slot (launches hold < 2^31 spans)
-};
-
-// Byte mask of word ww of chunk 0: its first h bytes are not the span's.
-WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {
-  return h >= 4u * ww + 4u ? 0u : (h <= 4u * ww ? ~0u : (~0u << (8u * (h - 4u * ww))));
-}
 
 // ---------------------------------------------------------------------------
 // The descriptor / strided / verify pipeline: the END-ALIGNED GRID.
@@ -277,43 +265,6 @@ WIPDB_LK_HD inline uint32_t PieceChunkOffset(uint32_t pw, uint32_t t) {
   const int32_t s0 = static_cast<int32_t>(4u * ((pw >> 12) & 3u));
   const int32_t b = 16 * (static_cast<int32_t>(t) - front);
   return static_cast<uint32_t>(b > s0 ? b : s0);
-}
-
-// ---- verify: the CRC residue ----
-// A verify span's grid ends jv <= 3 bytes past its stored trailer, so the
-// last 8 bytes of its last (or main) segment -- words 14 and 15 of lane 63's
-// last chunk -- hold the trailer at byte 4 - jv.  fix_trailer unmasks it in
-// place and zeroes the jv bytes after it; the register after the block ||
-// Unmask(trailer) || jv zero bytes is then the constant verify_residue(jv)
-// exactly when the trailer matches (feeding a word w: r -> zero-feed(r ^ w,
-// 4), and r ^ crc = ~0 for the register r = ~crc of the block; zero-feeds
-// are bijections), so no lane needs the trailer as a value.
-WIPDB_LK_HD constexpr uint32_t verify_residue(uint32_t jv) {
-  uint32_t r = ~0u;
-  for (uint32_t i = 0; i < 8u * (4u + jv); ++i) r = (r >> 1) ^ (0x82f63b78u & (0u - (r & 1u)));
-  return r;
-}
-WIPDB_LK_HD inline void fix_trailer(uint32_t& lo, uint32_t& hi, uint32_t jv) {
-  const uint64_t x = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
-  const uint32_t sh = 8u * (4u - jv);  // 8 .. 32
-  const uint32_t r = static_cast<uint32_t>(x >> sh) - 0xa282ead8u;
-  const uint32_t c = (r >> 17) | (r << 15);
-  const uint64_t y = (x & ((uint64_t(1) << sh) - 1u)) | (static_cast<uint64_t>(c) << sh);
-  lo = static_cast<uint32_t>(y);
-  hi = static_cast<uint32_t>(y >> 32);
-}
-
-// Chunk 0 of a span into its span form: read ws words late (shift right by
-// ws words), its hp leading bytes masked, the register inj entering at its
-// first byte.  Per lane.
-WIPDB_LK_HD inline void fix_head(uint32_t (&c)[4], uint32_t hp, uint32_t ws, uint32_t inj) {
-  uint32_t d[4];
-  d[3] = ws == 0u ? c[3] : (ws == 1u ? c[2] : (ws == 2u ? c[1] : c[0]));
-  d[2] = ws == 0u ? c[2] : (ws == 1u ? c[1] : (ws == 2u ? c[0] : 0u));
-  d[1] = ws == 0u ? c[1] : (ws == 1u ? c[0] : 0u);
-  d[0] = ws == 0u ? c[0] : 0u;
-  for (uint32_t w = 0; w < 4; ++w) c[w] = d[w] & head_mask(hp, w);
-  c[0] ^= inj;
 }
 
 }  // namespace lk
