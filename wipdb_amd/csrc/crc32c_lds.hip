@@ -223,6 +223,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     idx = uni(idx);
     const uint32_t ra = QRecAddr(idx);
     uint32_t r3 = 0;
+#pragma nounroll
     for (uint32_t spin = 0; spin < (1u << 22); ++spin) {  // its producer writes it next
       r3 = uni(lds_ld_sync(ra + 12u));
       if (r3 != 0u) break;
@@ -267,6 +268,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
                                               mbcnt_lo(static_cast<uint32_t>(lm), 0u)));
       // a slot is reused only once its last record has been read (256 slots,
       // at most 16 desks of 16 long spans in flight: this does not wait)
+#pragma nounroll
       for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
         const bool busy = lng && lds_ld_sync(ra + 12u) != 0u;
         if (ballot(busy) == 0u) break;
@@ -397,16 +399,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     nkind = kWNone;
     if (nstate == 0u && !exhausted) grab_desk();  // a desk ahead, loading
     for (int guard = 0; guard < 64; ++guard) {
-      if (rcnt != 0u && (rlanes >= 64u || rcnt == 64u)) {
-        issue_batch();
-        return;
-      }
+      if (rcnt != 0u && (rlanes >= 64u || rcnt == 64u)) break;  // a full batch
+      if (!lvalid && pfvalid) start_long();
       if (lvalid) {
-        issue_seg();
-        return;
-      }
-      if (pfvalid) {
-        start_long();
         issue_seg();
         return;
       }
@@ -416,46 +411,41 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       }
       pop();
       if (pfvalid) continue;
-      if (nstate != 0u) {  // (stalls on the desk's loads if they were issued just now)
-        switch_desk();
-        if (!exhausted) grab_desk();
-        continue;
-      }
-      break;
+      if (nstate == 0u) break;  // no work left but the ring's
+      // (stalls on the desk's loads if they were issued just now)
+      switch_desk();
+      if (!exhausted) grab_desk();
     }
     if (rcnt != 0u) issue_batch();
   };
-  // After an iteration: keep the next decide from stalling.
-  auto maintain = [&]() {
-    if (!pfvalid) pop();
-    if (dshort != 0u && rcnt < 64u) push_shorts();
-    if (dshort == 0u && !pfvalid && !lvalid && nstate == 2u) {
-      switch_desk();
-      if (!pfvalid) pop();
-      if (dshort != 0u && rcnt < 64u) push_shorts();
-    }
-  };
 
-  decide();
-  if (nkind == kWNone) return;
-  bool stored_prev = false;
+  // The loop: wait for this iteration's bytes, read them, issue the next
+  // iteration's DMA (decide), compute this one.  An iteration that ends the
+  // work may have pushed the last pieces: the loop then decides once more
+  // without an iteration in hand (that DMA goes out after its store, so the
+  // next wait is for everything).  One call site of decide: the kernel's
+  // code stays small.
+  bool have = false, stored_prev = false;
   for (;;) {
-    if (stored_prev) wait_vm<1>();
-    else wait_vm<0>();
-    if (nstate == 1u) nstate = 2u;  // the next desk's loads are in
-    ckind = nkind;
-    cs = ns;
-    cused = nused;
-    cb_pw = nb_pw;
-    cb_inj = nb_inj;
-    cb_id = nb_id;
-    cb_j = nb_j;
     uint32_t W[16];
-    pp.read(W);
     u32x4 ax{0, 0, 0, 0};
-    if (ckind == kWSeg && (cs.fl & kSAux))
-      ax = lds_ld4(SegAuxAddr(w));
-    pp.release();
+    if (have) {
+      if (stored_prev) wait_vm<1>();
+      else wait_vm<0>();
+      if (nstate == 1u) nstate = 2u;  // the next desk's loads are in
+      ckind = nkind;
+      cs = ns;
+      cused = nused;
+      cb_pw = nb_pw;
+      cb_inj = nb_inj;
+      cb_id = nb_id;
+      cb_j = nb_j;
+      pp.read(W);
+      if (ckind == kWSeg && (cs.fl & kSAux)) ax = lds_ld4(SegAuxAddr(w));
+      pp.release();
+    } else {
+      ckind = kWNone;
+    }
     decide();
 
     bool did_store = false;
@@ -559,14 +549,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       did_store = true;
     }
     stored_prev = did_store;
-    maintain();
+    if (have && !pfvalid) pop();  // the next long span, read while the DMA flies
     if (nkind == kWNone) {
-      // this iteration may have pushed the last pieces: their DMA goes out
-      // after its store, so the next wait is for everything
-      decide();
-      if (nkind == kWNone) break;
-      stored_prev = false;
+      if (!have) break;
+      have = false;
+      continue;
     }
+    have = true;
   }
 }
 
