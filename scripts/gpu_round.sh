@@ -1,0 +1,40 @@
+#!/bin/bash
+# GPU box: one call's worth of checks and measurements, each step under its
+# own time limit, stopping at the first step that faults / aborts / times out.
+#   STEPS="probe tests bench extra ab" PREFIX=r03a bash scripts/gpu_round.sh
+# Logs: gpurun_out/${PREFIX}_<step>.log (+ a summary in gpurun_out/steps.log).
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+P=${PREFIX:-r03}
+STEPS=${STEPS:-"probe tests bench extra"}
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/steps.log
+  local t0=$(date +%s)
+  timeout -k 10 "$to" "$@" > "gpurun_out/${P}_$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 )) s)" | tee -a gpurun_out/steps.log
+  grep -v "amdgpu.ids" "gpurun_out/${P}_$name.log" | tail -${TAILN:-6}
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    probe) run probe 200 python -u scripts/debug/lp_probe.py ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    testsall) run testsall 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;
+    benchq) run benchq 200 python bench.py --steps 50 --no-cpu-baseline ;;
+    extra) run extra 400 python scripts/bench_extra.py --what mixed,tblocks,vtblocks,verify ;;
+    mixed) run mixed 300 python scripts/bench_extra.py --what mixed ;;
+    host) run host 400 python scripts/bench_extra.py --what sst,host4k ;;
+    ab) run ab 600 bash scripts/gpu_abn.sh 2 tblocks,vtblocks,verify tree build/ab/lib_r02.so ;;
+    prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${P}_pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    pmc_write) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${P}_pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo ALLDONE
