@@ -77,6 +77,31 @@ def time_kernel(fn, stream, reps):
     return s.elapsed_time(e) / reps / 1e3
 
 
+def usable_cpus() -> int:
+    """CPUs this job may use (affinity, capped by OMP_NUM_THREADS: the GPU
+    box gives a one-GPU job 16 of its 256 CPUs)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, share) if share > 0 else n
+
+
+def cpu_rates(host, offs, lens):
+    """BASELINE config 3's CPU side: the library's host CRC path (SSE4.2
+    3-stream + PCLMUL combine, the reference's crc32c_3way class) over the
+    same spans from host memory, 1 thread and all usable CPUs, GiB/s."""
+    nbytes = float(lens.sum())
+    out = []
+    for threads in (1, usable_cpus()):
+        cpu_batch(host, offs, lens, threads=threads)  # warm
+        t0 = time.perf_counter()
+        cpu_batch(host, offs, lens, threads=threads)
+        out.append(round(nbytes / (time.perf_counter() - t0) / 2**30, 1))
+    return out
+
+
 def check_sample(host, offs, lens, got, rng, k=4000):
     idx = rng.choice(offs.size, min(k, offs.size), replace=False)
     want = cpu_batch(host, offs[idx], lens[idx])
@@ -123,8 +148,11 @@ def run_mixed(eng, d, stream, rng, gib):
                                                  split_small=SPLIT, split_long=SPLIT_LONG),
                     stream, 10)
     got = out.cpu().numpy().view(np.uint32)
+    cpu = cpu_rates(host, offs, lens)
+    res["cpu_threads"] = usable_cpus()
     res["mixed"] = {"spans": int(offs.size), "bytes": int(lens.sum()),
                     "GiBps": round(float(lens.sum()) / t / 2**30, 1),
+                    "cpu_1t_GiBps": cpu[0], "cpu_all_GiBps": cpu[1],
                     "mismatches_in_sample": check_sample(host, offs, lens, got, rng),
                     "sst_batch_latency": batch_latency(eng, dbuf, do, dl, stream)}
     for b in BUCKETS:  # one batch per bucket: same packing, only this size
@@ -136,8 +164,10 @@ def run_mixed(eng, d, stream, rng, gib):
                                                   split_long=SPLIT_LONG),
                          stream, 10)
         gotb = outb.cpu().numpy().view(np.uint32)
+        cpu = cpu_rates(host, ob, lb)
         res["buckets"][str(b)] = {"spans": int(ob.size),
                                   "GiBps": round(float(lb.sum()) / tb / 2**30, 1),
+                                  "cpu_1t_GiBps": cpu[0], "cpu_all_GiBps": cpu[1],
                                   "mismatches_in_sample": check_sample(host, ob, lb, gotb, rng,
                                                                        1000),
                                   "batch_latency": batch_latency(eng, dbuf, dob, dlb, stream,

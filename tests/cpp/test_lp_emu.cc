@@ -117,17 +117,19 @@ void RunVerify(const char* name, std::vector<uint8_t>& buf, const std::vector<ui
 }
 
 void RunStrided(const char* name, std::vector<uint8_t>& buf, uint64_t stride, uint32_t len,
-                uint32_t init, size_t n, uint32_t cus) {
+                uint32_t init, size_t n, uint32_t cus, bool mask = false) {
   std::vector<uint64_t> offs(n);
   std::vector<uint32_t> lens(n, len), want(n), got(n, 0x5A5A5A5Au);
   for (size_t i = 0; i < n; ++i) {
     offs[i] = i * stride;
     want[i] = Extend(init, buf.data() + offs[i], len);
+    if (mask) want[i] = wipdb::gf2::Mask(want[i]);
   }
   SetRange(buf);
   const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
   emu::launch(Grid(n, cus), [&] {
-    crc32c_lds_strided_kernel(buf.data(), stride, len, init, got.data(), n, 0u, img);
+    crc32c_lds_strided_kernel(buf.data(), stride, len, init, got.data(), n, mask ? kFlagMask : 0u,
+                              img);
   });
   Report(name, got, want, offs, lens);
 }
@@ -238,6 +240,9 @@ int main(int argc, char** argv) {
   if (Want(argc, argv, "strided")) {
     RunStrided("strided 4096", buf, 4096, 4096, 0, 1500, 3);
     RunStrided("strided 700 / 513 (init)", buf, 700, 513, 0x12345678u, 1500, 2);
+    RunStrided("strided 4096 masked", buf, 4096, 4096, 0, 255, 2, true);
+    RunStrided("strided 4101 / 4097 masked (init)", buf, 4101, 4097, 0x12345678u, 255, 2, true);
+    RunStrided("strided 4096 / 100 masked (init)", buf, 4096, 100, 7, 255, 2, true);
   }
   printf("%s: %d failing cases\n", g_fail ? "FAIL" : "PASS", g_fail);
   return g_fail ? 1 : 0;

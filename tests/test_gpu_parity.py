@@ -521,6 +521,37 @@ def test_full_size_4k_blocks(engine, oracle, reference):
     del dbuf
 
 
+def test_config4_shard_8m_blocks(engine, reference):
+    """BASELINE configs[3]'s per-GPU unit: 64 M x 4 KiB over 8 GPUs is 8 M
+    blocks (32 GiB) per device, the shard bench.py runs on every rank at
+    N > 1.  All 8 M CRCs are checked by the size-independent stitching
+    property (each pair of blocks as one 8 KiB span == Extend of the second
+    from the first's CRC: two independent computations, segments chained vs
+    separate launches), the descriptor and strided entry points agree on all
+    of them, and a 64 Ki-block sample is compared with the compiled
+    reference (oracle/_ref) on the host."""
+    import torch
+    nblk, bs, seed = 8 << 20, 4096, 0xC0F164
+    dbuf = torch.empty(nblk * bs, dtype=torch.uint8, device="cuda:0")
+    engine.fill_splitmix64_device(dbuf, seed)
+    offs = torch.arange(nblk, dtype=torch.int64, device="cuda:0") * bs
+    lens = torch.full((nblk,), bs, dtype=torch.int32, device="cuda:0")
+    spans_t = engine.batch_device(dbuf, offs, lens)
+    strided_t = engine.batch_strided_device(dbuf, bs, bs, nblk)
+    assert bool((spans_t == strided_t).all())
+    pair_t = engine.batch_device(dbuf, offs[::2].contiguous(),
+                                 torch.full((nblk // 2,), 2 * bs, dtype=torch.int32, device="cuda:0"))
+    chained_t = engine.batch_device(dbuf, offs[1::2].contiguous(), lens[1::2].contiguous(),
+                                    spans_t[::2].contiguous())
+    assert bool((pair_t == chained_t).all())
+    idx = torch.from_numpy(np.random.default_rng(4).choice(nblk, 1 << 16, replace=False)).to("cuda:0")
+    sample = dbuf.view(nblk, bs).index_select(0, idx).cpu().numpy().reshape(-1)
+    want = reference.batch(sample, np.arange(1 << 16, dtype=np.uint64) * bs,
+                           np.full(1 << 16, bs, np.uint32), threads=8)
+    np.testing.assert_array_equal(_u32(spans_t.index_select(0, idx)), want)
+    del dbuf, pair_t, chained_t
+
+
 def test_masked_strided_and_init(engine, oracle):
     import torch
     rng = np.random.default_rng(21)

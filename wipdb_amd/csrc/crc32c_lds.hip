@@ -128,7 +128,7 @@ struct SegW {
 // What an iteration computes.
 constexpr uint32_t kWNone = 0u, kWSeg = 1u, kWBatch = 2u;
 
-template <int OUT, bool kInit, typename Src>
+template <int OUT, typename Src>
 __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags,
                                        const uint8_t* image) {
   constexpr bool kV = OUT == 1;
@@ -238,7 +238,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     pfa = (static_cast<uint64_t>(r1) << 32) | r0;
     pfn = r2;
     pfid = r3 - 1u;
-    pfinit = kInit ? src.init_of(pfid) : 0u;
+    pfinit = src.init_of(pfid);  // (0 without an init column; the strided blocks' init)
     pfvalid = true;
   };
 
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u};
-  run_lp<0, INIT != 0>(src, out, flags, image);
+  run_lp<0>(src, out, flags, image);
 }
 template __global__ void crc32c_lds_spans_kernel<0>(const uint8_t*, const uint64_t*,
                                                     const uint32_t*, const uint32_t*, uint32_t*,
@@ -584,7 +584,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t length, uint32_t init,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const StridedSrc src{base, stride, length, init, count};
-  run_lp<0, false>(src, out, flags & kFlagMask, image);
+  run_lp<0>(src, out, flags & kFlagMask, image);
 }
 
 // Read-side verify (ReadBlock, kv/src/table/format.cc:91-99): block i =
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
     const uint8_t* __restrict__ image) {
   const DescSrc<false> src{base, offsets, lengths, nullptr, count, 1u};
-  run_lp<1, false>(src, status, 0u, image);
+  run_lp<1>(src, status, 0u, image);
 }
 
 }  // namespace lk
