@@ -166,7 +166,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint64_t dbase = 0, nbase = 0;
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
   uint32_t nlive = 0;         // next desk: lanes holding a span
+  uint32_t nshort = 0;        // next desk: its short spans (once published)
   uint32_t nstate = 0;        // next desk: 0 none, 1 loads issued, 2 loads waited for
+  bool npub = false;          // next desk: long spans queued, empty spans answered
   bool exhausted = false;
   // ---- the long span being run, and the next one (taken from the queue) ----
   Plan lsp{};
@@ -198,7 +200,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const bool v = l < 16u && s < count;
     nlive = static_cast<uint32_t>(ballot(v));
     if (v) src.lane(s, na, nn, ni);
+    if (l == 0u) lds_add(MiscAddr(kMiscDesks), 1u);
     nstate = 1;
+    npub = false;
   };
 
   // The long-span queue (workgroup, LDS).  pop: claim the head record by CAS
@@ -242,32 +246,28 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     pfvalid = true;
   };
 
-  // The next desk becomes the desk: empty spans answered, long spans into
-  // the workgroup's queue, short ones marked for the ring.
-  auto switch_desk = [&]() {
-    da = na;
-    dn = nn;
-    di = ni;
-    dbase = nbase;
+  // The next desk's long spans into the workgroup's queue (as soon as its
+  // descriptors are in: other waves may be waiting for work), its empty
+  // spans answered; its short spans wait for the switch.
+  auto publish_desk = [&]() {
     const bool live = l < 16u && ((nlive >> (l & 15u)) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
-    nstate = 0;
-    const uint64_t s = dbase + l;
-    const Plan p = MakePlan(da, static_cast<uint32_t>(sbase + da), dn, kV);
+    const uint64_t s = nbase + l;
+    const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), nn, kV);
     const bool empty = live && p.empty;
     const bool lng = live && !p.empty && p.m != 0u;
     const bool sht = live && !p.empty && p.m == 0u;
-    if (!kV && empty) out32[s] = msk ? mask_crc(di) : di;
-    dshort = static_cast<uint32_t>(ballot(sht));
+    if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
+    nshort = static_cast<uint32_t>(ballot(sht));
     const uint64_t lm = ballot(lng);
     if (lm != 0u) {
       uint32_t base = 0;
       if (l == 0u) base = lds_add(MiscAddr(kMiscQTail), static_cast<uint32_t>(__builtin_popcountll(lm)));
       base = uni(base);
-      const uint32_t ra = QRecAddr(base + mbcnt_hi(
-                                              static_cast<uint32_t>(lm >> 32),
-                                              mbcnt_lo(static_cast<uint32_t>(lm), 0u)));
-      // a slot is reused only once its last record has been read (256 slots,
-      // at most 16 desks of 16 long spans in flight: this does not wait)
+      const uint32_t ra = QRecAddr(base + mbcnt_hi(static_cast<uint32_t>(lm >> 32),
+                                                   mbcnt_lo(static_cast<uint32_t>(lm), 0u)));
+      // a slot is reused only once its last record has been read (256 slots;
+      // a wave queues a desk only after it found the queue empty, so at most
+      // 16 desks of 16 long spans are in it: this does not wait)
 #pragma nounroll
       for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
         const bool busy = lng && lds_ld_sync(ra + 12u) != 0u;
@@ -275,13 +275,26 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         lk_sleep();
       }
       if (lng) {
-        lds_st_sync(ra, static_cast<uint32_t>(da));
-        lds_st_sync(ra + 4u, static_cast<uint32_t>(da >> 32));
-        lds_st_sync(ra + 8u, dn);
+        lds_st_sync(ra, static_cast<uint32_t>(na));
+        lds_st_sync(ra + 4u, static_cast<uint32_t>(na >> 32));
+        lds_st_sync(ra + 8u, nn);
       }
       lgkm_wait();  // the record before its marker
       if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(s) + 1u);
     }
+    lgkm_wait();  // queued before the in-flight count drops
+    if (l == 0u) lds_add(MiscAddr(kMiscDesks), 0xffffffffu);
+    npub = true;
+  };
+  // The next desk becomes the desk (its short spans for the ring).
+  auto switch_desk = [&]() {
+    if (!npub) publish_desk();
+    da = na;
+    dn = nn;
+    di = ni;
+    dbase = nbase;
+    dshort = nshort;
+    nstate = 0;
   };
 
   // The desk's short spans into the ring, as many as it has room for.
@@ -411,10 +424,32 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       }
       pop();
       if (pfvalid) continue;
-      if (nstate == 0u) break;  // no work left but the ring's
-      // (stalls on the desk's loads if they were issued just now)
-      switch_desk();
-      if (!exhausted) grab_desk();
+      if (nstate != 0u) {
+        // (stalls on the desk's loads if they were issued just now)
+        switch_desk();
+        if (!exhausted) grab_desk();
+        continue;
+      }
+      if (rcnt != 0u) break;  // the ring's last pieces
+      // nothing of this wave's own: a desk another wave grabbed may still
+      // queue long spans -- wait for it (bounded) rather than leave them to
+      // that wave alone
+      bool again = false;
+#pragma nounroll
+      for (uint32_t spin = 0; spin < (1u << 16); ++spin) {
+        if (uni(lds_ld_sync(MiscAddr(kMiscDesks))) == 0u) {
+          pop();
+          again = pfvalid;
+          break;
+        }
+        lk_sleep();
+        pop();
+        if (pfvalid) {
+          again = true;
+          break;
+        }
+      }
+      if (!again) break;
     }
     if (rcnt != 0u) issue_batch();
   };
@@ -549,7 +584,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       did_store = true;
     }
     stored_prev = did_store;
-    if (have && !pfvalid) pop();  // the next long span, read while the DMA flies
+    if (have) {
+      // while the DMA flies: queue the next desk's long spans once it is in,
+      // and take the next long span when this one is about to end (not
+      // earlier: another wave may be idle)
+      if (nstate == 2u && !npub) publish_desk();
+      if (!pfvalid && (!lvalid || lt + 1u >= lsp.m)) pop();
+    }
     if (nkind == kWNone) {
       if (!have) break;
       have = false;
