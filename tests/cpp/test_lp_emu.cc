@@ -197,6 +197,13 @@ int main(int argc, char** argv) {
     auto l = lens_of(3000, 512, 576);
     RunSpans("512 bucket packed", buf, Packed(l, 3, 5), l, nullptr, true, 4);
   }
+  if (Want(argc, argv, "1-2 KiB buckets")) {  // pieces of 16..58 lanes: most split over two batches
+    auto l = lens_of(1500, 1024, 1152);
+    RunSpans("1 KiB bucket packed", buf, Packed(l, 1, 5), l, nullptr, false, 3);
+    auto l2 = lens_of(1500, 2048, 3700);
+    auto in = inits_of(l2.size());
+    RunSpans("2-3.6 KiB packed (inits)", buf, Packed(l2, 6, 5), l2, &in, true, 3);
+  }
   if (Want(argc, argv, "aligned 4 KiB")) {
     std::vector<uint64_t> o;
     for (int i = 0; i < 2000; ++i) o.push_back(4096u * i);

@@ -182,6 +182,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   SegW cs{}, ns{};
   uint32_t cb_pw = 0, cb_inj = 0, cb_id = 0, cb_j = 0;  // batch, per lane
   uint32_t nb_pw = 0, nb_inj = 0, nb_id = 0, nb_j = 0;
+  uint32_t csplit = 64, nsplit = 64;  // a batch's split piece: its first lane (64: none)
+  uint32_t carry = 0, carry_tw = 0;   // the split piece's register over its first lanes, tail word
   uint32_t chain = 0;
 
   // A desk of 16 spans: one unit-counter add, the descriptors loaded (lanes
@@ -352,17 +354,24 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     ++lt;
     if (last) lvalid = false;
   };
+  // A batch: the ring's first pieces, each on its remaining lanes, in order;
+  // the batch fills all 64 lanes -- a piece that does not fit is split, its
+  // first lanes now and the rest (a continuation, its register carried) at
+  // the head of the next batch.
   auto issue_batch = [&]() {
-    const uint32_t nlq = l < rcnt ? PW{rpw}.nl() : 0u;
-    const uint32_t incl = scan_add(nlq, l);
+    const PW rw{rpw};
+    const uint32_t rem = l < rcnt ? rw.rem() : 0u;
+    const uint32_t incl = scan_add(rem, l);
     const bool tk = l < rcnt && incl <= 64u;
-    const uint64_t tm = ballot(tk);
-    const uint32_t n = static_cast<uint32_t>(__builtin_popcountll(tm));  // >= 1
-    const uint32_t used = rdlane(incl, n - 1u);
-    const uint32_t st = incl - nlq;
+    const uint32_t n = static_cast<uint32_t>(__builtin_popcountll(ballot(tk)));  // >= 1
+    const uint32_t usedf = rdlane(incl, n - 1u);
+    const bool part = usedf < 64u && n < rcnt;  // entry n is split
+    const uint32_t used = part ? 64u : usedf;
+    const uint32_t st = incl - rem;
     // start lanes of the taken pieces, and each lane's piece
-    const uint32_t smlo = scan_or(tk && st < 32u ? 1u << (st & 31u) : 0u);
-    const uint32_t smhi = scan_or(tk && st >= 32u ? 1u << (st & 31u) : 0u);
+    const bool sb = tk || (part && l == n);
+    const uint32_t smlo = scan_or(sb && st < 32u ? 1u << (st & 31u) : 0u);
+    const uint32_t smhi = scan_or(sb && st >= 32u ? 1u << (st & 31u) : 0u);
     const uint32_t le = mbcnt_hi(smhi, mbcnt_lo(smlo, 0u)) +
                         (((l < 32u ? smlo : smhi) >> (l & 31u)) & 1u);
     const uint32_t e = le - 1u;
@@ -370,8 +379,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t b_lo = bperm(rp_lo, e), b_hi = bperm(rp_hi, e);
     const uint32_t b_pw = bperm(rpw, e), b_inj = bperm(rinj, e), b_id = bperm(rid, e);
     const uint32_t b_st = bperm(st, e);
-    const uint32_t j = live ? l - b_st : 0u;
     const PW pw{live ? b_pw : 0u};
+    const uint32_t j = live ? pw.j0() + (l - b_st) : 0u;  // the lane's stripe of its piece
     const Stripe sp = MakeStripe(pw, j);
     const uint64_t S = sbase + ((static_cast<uint64_t>(b_hi) << 32) | b_lo) +
                        static_cast<uint64_t>(sp.s);
@@ -389,13 +398,15 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     nb_id = b_id;
     nb_j = j;
     nused = used;
+    nsplit = part ? usedf : 64u;
     nkind = kWBatch;
-    // the ring drops its first n entries
+    // the ring drops its first n entries; a split one stays at its head
     rp_lo = bperm(rp_lo, l + n);
     rp_hi = bperm(rp_hi, l + n);
     rpw = bperm(rpw, l + n);
     rinj = bperm(rinj, l + n);
     rid = bperm(rid, l + n);
+    if (part && l == 0u) rpw = PW{rpw}.advanced(64u - usedf);
     rcnt -= n;
     rlanes -= used;
   };
@@ -475,6 +486,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       cb_inj = nb_inj;
       cb_id = nb_id;
       cb_j = nb_j;
+      csplit = nsplit;
       pp.read(W);
       if (ckind == kWSeg && (cs.fl & kSAux)) ax = lds_ld4(SegAuxAddr(w));
       pp.release();
@@ -565,21 +577,35 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         W[15] = lastl ? hi : W[15];
       }
       const uint32_t R = scan(lk, W);
-      const uint32_t v = shift64(lk, k1b, k2b, R, live ? nl - 1u - j : 0u);
+      const uint32_t d = live ? nl - 1u - j : 0u;  // lanes of the piece after this one
+      const uint32_t v = shift64(lk, k1b, k2b, R, d);
       const uint32_t xs = scan_xor(v, l);
-      uint32_t G = bperm(xs, l + nl - 1u) ^ xs ^ v;  // the piece's register, at its lane 0
+      // the piece's lanes in this batch end at lane l + min(d, 63 - l): the
+      // XOR over them, at its first lane here (j == j0)
+      const uint32_t last = l + (d < 63u - l ? d : 63u - l);
+      uint32_t G = bperm(xs, last) ^ xs ^ v;
+      const bool leader = live && j == pw.j0();
+      const bool done = d <= 63u - l;  // (at the leader) the piece ends in this batch
+      // a continuation finishes with the register carried from its first
+      // lanes (and their tail word); a split piece leaves its own for the next
+      const uint32_t c_new = csplit < 64u ? rdlane(G, csplit) : 0u;
+      const uint32_t t_new = csplit < 64u ? rdlane(tw, csplit) : 0u;
+      G ^= pw.cont() ? carry : 0u;
+      const uint32_t twv = pw.cont() ? carry_tw : tw;
       G ^= r == 0u ? cb_inj : 0u;
-      const bool leader = live && j == 0u;
+      carry = c_new;
+      carry_tw = t_new;
+      const bool fin = leader && done;
       if (kV) {
         constexpr uint32_t kRes0 = verify_residue(0), kRes1 = verify_residue(1),
                            kRes2 = verify_residue(2), kRes3 = verify_residue(3);
         const uint32_t jv = pw.jv();
         const uint32_t res = jv == 0u ? kRes0 : (jv == 1u ? kRes1 : (jv == 2u ? kRes2 : kRes3));
-        if (leader) out8[cb_id] = G == res ? 1u : 0u;
+        if (fin) out8[cb_id] = G == res ? 1u : 0u;
       } else {
-        const uint32_t Gt = tail_step(lk, G, tw, pw.k());
+        const uint32_t Gt = tail_step(lk, G, twv, pw.k());
         G = pw.x() ? Gt : G;
-        if (leader) out32[cb_id] = msk ? mask_crc(~G) : ~G;
+        if (fin) out32[cb_id] = msk ? mask_crc(~G) : ~G;
       }
       did_store = true;
     }

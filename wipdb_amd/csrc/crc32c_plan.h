@@ -58,12 +58,15 @@ WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {
 
 // ---- piece word: the packed geometry of a piece (ring entry) ----
 //   r (8) | x << 8 | hp (4) << 9 | ws (2) << 13 | te (4) << 15 | k (2) << 19 |
-//   jv (2) << 21
+//   jv (2) << 21 | cont << 23 | j0 (6) << 24
 // r: the piece's chunks; x: the aux chunk is read (the span has a tail);
 // hp / ws: head bytes masked / words read late (a whole-span piece only);
 // te: the byte of the aux chunk where the tail word starts (the aux chunk
 // is the 16 bytes at E4 - te); k: tail bytes; jv: verify grid bytes past
-// the trailer.  The piece's first real chunk is at p0 = E4 - 16 r.
+// the trailer.  The piece's first real chunk is at p0 = E4 - 16 r.  cont /
+// j0: the kernel split the piece over two batch iterations and lanes
+// [j0, nl) of it are still to come (the register of lanes [0, j0) is carried).
+constexpr uint32_t kPWCont = 1u << 23;
 struct PW {
   uint32_t v;
   WIPDB_LK_HD inline uint32_t r() const { return v & 0xffu; }
@@ -73,9 +76,16 @@ struct PW {
   WIPDB_LK_HD inline uint32_t te() const { return (v >> 15) & 15u; }
   WIPDB_LK_HD inline uint32_t k() const { return (v >> 19) & 3u; }
   WIPDB_LK_HD inline uint32_t jv() const { return (v >> 21) & 3u; }
+  WIPDB_LK_HD inline bool cont() const { return (v & kPWCont) != 0u; }
+  WIPDB_LK_HD inline uint32_t j0() const { return (v >> 24) & 63u; }
   // lanes of the piece, and its window chunks in front of it
   WIPDB_LK_HD inline uint32_t nl() const { return (r() + x() + 3u) >> 2; }
   WIPDB_LK_HD inline uint32_t front() const { return 4u * nl() - r(); }
+  // lanes still to come, and the word once `taken` more of them were batched
+  WIPDB_LK_HD inline uint32_t rem() const { return nl() - j0(); }
+  WIPDB_LK_HD inline uint32_t advanced(uint32_t taken) const {
+    return (v & ~(63u << 24)) | kPWCont | ((j0() + taken) << 24);
+  }
 };
 WIPDB_LK_HD inline uint32_t PackPW(uint32_t r, uint32_t x, uint32_t hp, uint32_t ws, uint32_t te,
                                    uint32_t k, uint32_t jv) {
