@@ -140,6 +140,8 @@ inline void lds_st_sync(uint32_t a, uint32_t v) { __atomic_store_n(lds_w(a), v, 
 // not overwrite a slot another lane has yet to read)
 inline void lgkm_wait() { emu::wave().bar.wait(); }
 inline void compiler_barrier() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+template <class T>
+inline void loads_landed(T&) {}
 
 // ---- lanes ----
 inline uint32_t lane_tid() { return emu::t_tid; }

@@ -224,12 +224,15 @@ struct DescSrc {
   __device__ __forceinline__ SpanD get(uint64_t s) const {
     return SpanD{off[s], len[s] + extra, kInit ? init[s] : 0u, static_cast<uint32_t>(s)};
   }
-  // per lane (a desk of run_lp): vector loads, waited for at first use
+  // per lane (a desk of run_lp): vector loads, waited for at first use --
+  // n is the length column as loaded (bytes(n) adds the type byte: no
+  // arithmetic on a load still in flight)
   __device__ __forceinline__ void lane(uint64_t s, uint64_t& a, uint32_t& n, uint32_t& i) const {
     a = off[s];
-    n = len[s] + extra;
+    n = len[s];
     i = kInit ? init[s] : 0u;
   }
+  __device__ __forceinline__ uint32_t bytes(uint32_t n) const { return n + extra; }
   __device__ __forceinline__ uint32_t init_of(uint64_t s) const { return kInit ? init[s] : 0u; }
 };
 
@@ -247,6 +250,7 @@ struct StridedSrc {
     n = length;
     i = init;
   }
+  __device__ __forceinline__ uint32_t bytes(uint32_t n) const { return n; }
   __device__ __forceinline__ uint32_t init_of(uint64_t) const { return init; }
 };
 

@@ -254,7 +254,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   auto publish_desk = [&]() {
     const bool live = l < 16u && ((nlive >> (l & 15u)) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
     const uint64_t s = nbase + l;
-    const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), nn, kV);
+    const uint32_t nb = src.bytes(nn);
+    const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), nb, kV);
     const bool empty = live && p.empty;
     const bool lng = live && !p.empty && p.m != 0u;
     const bool sht = live && !p.empty && p.m == 0u;
@@ -279,7 +280,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       if (lng) {
         lds_st_sync(ra, static_cast<uint32_t>(na));
         lds_st_sync(ra + 4u, static_cast<uint32_t>(na >> 32));
-        lds_st_sync(ra + 8u, nn);
+        lds_st_sync(ra + 8u, nb);
       }
       lgkm_wait();  // the record before its marker
       if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(s) + 1u);
@@ -292,7 +293,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   auto switch_desk = [&]() {
     if (!npub) publish_desk();
     da = na;
-    dn = nn;
+    dn = src.bytes(nn);
     di = ni;
     dbase = nbase;
     dshort = nshort;
@@ -421,7 +422,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // Chooses and issues the next iteration (nkind = kWNone: no work left).
   auto decide = [&]() {
     nkind = kWNone;
-    if (nstate == 0u && !exhausted) grab_desk();  // a desk ahead, loading
     for (int guard = 0; guard < 64; ++guard) {
       if (rcnt != 0u && (rlanes >= 64u || rcnt == 64u)) break;  // a full batch
       if (!lvalid && pfvalid) start_long();
@@ -438,10 +438,16 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       if (nstate != 0u) {
         // (stalls on the desk's loads if they were issued just now)
         switch_desk();
-        if (!exhausted) grab_desk();
         continue;
       }
       if (rcnt != 0u) break;  // the ring's last pieces
+      if (!exhausted) {
+        grab_desk();  // (a stall: nothing else to do)
+        loads_landed(na);
+        loads_landed(nn);
+        loads_landed(ni);
+        continue;
+      }
       // nothing of this wave's own: a desk another wave grabbed may still
       // queue long spans -- wait for it (bounded) rather than leave them to
       // that wave alone
@@ -493,6 +499,10 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     } else {
       ckind = kWNone;
     }
+    // (no path into decide carries a desk load in flight: see loads_landed)
+    loads_landed(na);
+    loads_landed(nn);
+    loads_landed(ni);
     decide();
 
     bool did_store = false;
@@ -617,8 +627,15 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       if (nstate == 2u && !npub) publish_desk();
       if (!pfvalid && (!lvalid || lt + 1u >= lsp.m)) pop();
     }
+    // the next desk's descriptor loads go out after this iteration's DMA and
+    // store: the wait for that DMA covers them (nothing in decide waits on
+    // them with the next DMA not yet issued)
+    if (nstate == 0u && !exhausted) grab_desk();
     if (nkind == kWNone) {
-      if (!have) break;
+      // (decide gives up after 64 steps -- e.g. desks of empty spans -- with
+      // work left: decide again)
+      const bool left = nstate != 0u || !exhausted || dshort != 0u || rcnt != 0u || lvalid || pfvalid;
+      if (!have && !left) break;
       have = false;
       continue;
     }

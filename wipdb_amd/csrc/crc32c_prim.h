@@ -47,6 +47,12 @@ __device__ __forceinline__ void lds_st_sync(uint32_t a, uint32_t v) {
 // every LDS access of this wave has completed (and none moves across)
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void compiler_barrier() { asm volatile("" ::: "memory"); }
+// v was loaded from global memory and that load is known to be complete
+// (a wait on the DMA issued after it): an asm use makes the compiler place
+// its own wait for the load here, where it costs nothing, and not at a later
+// register copy -- where it would also wait for a DMA issued in between.
+template <class T>
+__device__ __forceinline__ void loads_landed(T& v) { asm volatile("" : "+v"(v)); }
 
 // ---- lanes ----
 __device__ __forceinline__ uint32_t lane_tid() { return threadIdx.x; }
