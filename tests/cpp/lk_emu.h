@@ -142,6 +142,7 @@ inline void lgkm_wait() { emu::wave().bar.wait(); }
 inline void compiler_barrier() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 template <class T>
 inline void loads_landed(T&) {}
+inline uint32_t vzero() { return 0u; }
 
 // ---- lanes ----
 inline uint32_t lane_tid() { return emu::t_tid; }

@@ -233,7 +233,10 @@ struct DescSrc {
     i = kInit ? init[s] : 0u;
   }
   __device__ __forceinline__ uint32_t bytes(uint32_t n) const { return n + extra; }
-  __device__ __forceinline__ uint32_t init_of(uint64_t s) const { return kInit ? init[s] : 0u; }
+  // (a vector load: see vzero)
+  __device__ __forceinline__ uint32_t init_of(uint64_t s) const {
+    return kInit ? init[s + vzero()] : 0u;
+  }
 };
 
 // Fixed-size blocks at a fixed stride.

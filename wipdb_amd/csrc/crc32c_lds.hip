@@ -434,6 +434,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         continue;
       }
       pop();
+      loads_landed(pfinit);
       if (pfvalid) continue;
       if (nstate != 0u) {
         // (stalls on the desk's loads if they were issued just now)
@@ -456,11 +457,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       for (uint32_t spin = 0; spin < (1u << 16); ++spin) {
         if (uni(lds_ld_sync(MiscAddr(kMiscDesks))) == 0u) {
           pop();
+          loads_landed(pfinit);
           again = pfvalid;
           break;
         }
         lk_sleep();
         pop();
+        loads_landed(pfinit);
         if (pfvalid) {
           again = true;
           break;
@@ -503,6 +506,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     loads_landed(na);
     loads_landed(nn);
     loads_landed(ni);
+    loads_landed(pfinit);
     decide();
 
     bool did_store = false;

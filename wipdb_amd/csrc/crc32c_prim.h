@@ -53,6 +53,10 @@ __device__ __forceinline__ void compiler_barrier() { asm volatile("" ::: "memory
 // register copy -- where it would also wait for a DMA issued in between.
 template <class T>
 __device__ __forceinline__ void loads_landed(T& v) { asm volatile("" : "+v"(v)); }
+// 0, but lane-varying to the compiler: a load from a uniform address made
+// a vector load (its wait is a vmcnt one, ordered with the DMA, not an lgkmcnt
+// one that every later LDS access would also wait for)
+__device__ __forceinline__ uint32_t vzero() { return __builtin_amdgcn_mbcnt_lo(0u, 0u); }
 
 // ---- lanes ----
 __device__ __forceinline__ uint32_t lane_tid() { return threadIdx.x; }
