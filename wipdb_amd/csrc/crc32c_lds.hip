@@ -128,6 +128,17 @@ struct SegW {
 // What an iteration computes.
 constexpr uint32_t kWNone = 0u, kWSeg = 1u, kWBatch = 2u;
 
+#if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
+// Profiling build only: per wave, the cycles of each part of run_lp's loop
+// (s_memtime) and its iteration counts, summed over launches.
+__device__ unsigned long long g_lp_prof[4096 * 8];
+#define LP_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
+#define LP_ACC(k, v) (prof[k] += (v))
+#else
+#define LP_T(x)
+#define LP_ACC(k, v)
+#endif
+
 template <int OUT, typename Src>
 __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags,
                                        const uint8_t* image) {
@@ -481,7 +492,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // next wait is for everything).  One call site of decide: the kernel's
   // code stays small.
   bool have = false, stored_prev = false;
+#if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  LP_T(t_start);
+#endif
   for (;;) {
+    LP_T(t0);
     uint32_t W[16];
     u32x4 ax{0, 0, 0, 0};
     if (have) {
@@ -507,7 +523,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     loads_landed(nn);
     loads_landed(ni);
     loads_landed(pfinit);
+    LP_T(t1);
     decide();
+    LP_T(t2);
 
     bool did_store = false;
     if (ckind == kWSeg) {
@@ -624,6 +642,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       did_store = true;
     }
     stored_prev = did_store;
+    LP_T(t3);
     if (have) {
       // while the DMA flies: queue the next desk's long spans once it is in,
       // and take the next long span when this one is about to end (not
@@ -635,6 +654,14 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     // store: the wait for that DMA covers them (nothing in decide waits on
     // them with the next DMA not yet issued)
     if (nstate == 0u && !exhausted) grab_desk();
+    LP_T(t4);
+    LP_ACC(0, t1 - t0);
+    LP_ACC(1, t2 - t1);
+    LP_ACC(2, t3 - t2);
+    LP_ACC(3, t4 - t3);
+    LP_ACC(4, ckind == kWSeg ? 1u : 0u);
+    LP_ACC(5, ckind == kWBatch ? 1u : 0u);
+    LP_ACC(6, ckind == kWNone ? 1u : 0u);
     if (nkind == kWNone) {
       // (decide gives up after 64 steps -- e.g. desks of empty spans -- with
       // work left: decide again)
@@ -645,6 +672,14 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     }
     have = true;
   }
+#if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
+  LP_T(t_end);
+  prof[7] = t_end - t_start;
+  if (l == 0u) {
+    const uint32_t slot = (group_id() * static_cast<uint32_t>(kWaves) + w) & 4095u;
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_lp_prof[slot * 8u + k], static_cast<unsigned long long>(prof[k]));
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -688,3 +723,19 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
 
 }  // namespace lk
 }  // namespace wipdb
+
+#if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
+// Profiling build only: copies (and with reset != 0 zeroes) g_lp_prof.
+extern "C" __attribute__((visibility("default"))) int hcrc_debug_lp_prof(void* host, uint64_t bytes,
+                                                                          int reset) {
+  if (bytes > sizeof(unsigned long long) * 4096 * 8) return -1;
+  if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(wipdb::lk::g_lp_prof), bytes) != hipSuccess)
+    return -2;
+  if (reset) {
+    static unsigned long long zero[4096 * 8];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(wipdb::lk::g_lp_prof), zero, sizeof(zero)) != hipSuccess)
+      return -3;
+  }
+  return 0;
+}
+#endif
