@@ -222,6 +222,14 @@ int main(int argc, char** argv) {
     auto l = lens_of(300, 8000, 70000);
     RunSpans("long 8..70 KiB", buf, Packed(l, 2, 5), l, nullptr, false, 2);
   }
+  if (Want(argc, argv, "shared long")) {  // one wave's desks of long spans, the others idle: shared
+    auto l = lens_of(16, 20000, 70000);
+    auto in = inits_of(l.size());
+    RunSpans("shared long: one desk (inits)", buf, Packed(l, 3, 5), l, &in, false, 1);
+    auto l2 = lens_of(40, 8000, 300000);
+    auto in2 = inits_of(l2.size());
+    RunSpans("shared long: 40 (inits)", buf, Packed(l2, 1, 5), l2, &in2, true, 2);
+  }
   if (Want(argc, argv, "zipf mix")) {
     const uint32_t B[] = {512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
     std::vector<uint32_t> l;

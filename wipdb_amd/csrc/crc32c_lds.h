@@ -68,7 +68,9 @@ constexpr uint32_t kMiscHead0 = 256;   // 16 words: ~0 * x^(-8h)
 constexpr uint32_t kMiscUnit = 272;    // the workgroup's unit counter
 constexpr uint32_t kMiscQHead = 273;   // the long-span queue's head / tail (run_lp)
 constexpr uint32_t kMiscQTail = 274;
-constexpr uint32_t kMiscDesks = 275;   // desks grabbed whose long spans are not queued yet
+constexpr uint32_t kMiscDesks = 275;   // desks grabbed, not sorted yet (run_lp)
+constexpr uint32_t kMiscIdle = 276;    // waves out of work, waiting for shared long spans
+constexpr uint32_t kMiscHeld = 277;    // long spans held by a wave, not taken or shared yet
 constexpr uint32_t kMiscBytes = 1024 * 4;
 
 // run_lp (the lane-packed spans / strided / verify kernels):

@@ -176,10 +176,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
   uint64_t dbase = 0, nbase = 0;
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
+  uint32_t dlong = 0;         // desk lanes whose long span this wave has not taken
   uint32_t nlive = 0;         // next desk: lanes holding a span
-  uint32_t nshort = 0;        // next desk: its short spans (once published)
+  uint32_t nshort = 0, nlong = 0;  // next desk: its short / long spans (once sorted)
   uint32_t nstate = 0;        // next desk: 0 none, 1 loads issued, 2 loads waited for
-  bool npub = false;          // next desk: long spans queued, empty spans answered
+  bool nsorted = false;       // next desk: sorted (empty spans answered)
   bool exhausted = false;
   // ---- the long span being run, and the next one (taken from the queue) ----
   Plan lsp{};
@@ -215,11 +216,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (v) src.lane(s, na, nn, ni);
     if (l == 0u) lds_add(MiscAddr(kMiscDesks), 1u);
     nstate = 1;
-    npub = false;
+    nsorted = false;
   };
 
-  // The long-span queue (workgroup, LDS).  pop: claim the head record by CAS
-  // while head < tail, read it once its producer has written it, free it.
+  // The long-span queue (workgroup, LDS): a wave's own long spans go there
+  // only when another wave has run out of work (share).  pop: claim the head
+  // record by CAS while head < tail, read it once its producer has written
+  // it, free it.
   auto pop = [&]() {
     uint32_t got = 0, idx = 0;
     if (l == 0u) {
@@ -258,56 +261,81 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     pfinit = src.init_of(pfid);  // (0 without an init column; the strided blocks' init)
     pfvalid = true;
   };
-
-  // The next desk's long spans into the workgroup's queue (as soon as its
-  // descriptors are in: other waves may be waiting for work), its empty
-  // spans answered; its short spans wait for the switch.
-  auto publish_desk = [&]() {
-    const bool live = l < 16u && ((nlive >> (l & 15u)) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
-    const uint64_t s = nbase + l;
-    const uint32_t nb = src.bytes(nn);
-    const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), nb, kV);
-    const bool empty = live && p.empty;
-    const bool lng = live && !p.empty && p.m != 0u;
-    const bool sht = live && !p.empty && p.m == 0u;
-    if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
-    nshort = static_cast<uint32_t>(ballot(sht));
-    const uint64_t lm = ballot(lng);
-    if (lm != 0u) {
-      uint32_t base = 0;
-      if (l == 0u) base = lds_add(MiscAddr(kMiscQTail), static_cast<uint32_t>(__builtin_popcountll(lm)));
-      base = uni(base);
-      const uint32_t ra = QRecAddr(base + mbcnt_hi(static_cast<uint32_t>(lm >> 32),
-                                                   mbcnt_lo(static_cast<uint32_t>(lm), 0u)));
-      // a slot is reused only once its last record has been read (256 slots;
-      // a wave queues a desk only after it found the queue empty, so at most
-      // 16 desks of 16 long spans are in it: this does not wait)
+  // The long spans of desk lanes m (a, bytes b, span base + lane) into the
+  // queue; they leave the workgroup's held count once queued.
+  auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint64_t base) {
+    const bool lng = l < 16u && ((m >> (l & 15u)) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
+    const uint32_t k = static_cast<uint32_t>(__builtin_popcount(m));
+    uint32_t q = 0;
+    if (l == 0u) q = lds_add(MiscAddr(kMiscQTail), k);
+    q = uni(q);
+    const uint32_t ra = QRecAddr(q + mbcnt_lo(m, 0u));
+    // a slot is reused only once its last record has been read (queue
+    // records are popped by the waves that asked for work: this rarely waits)
 #pragma nounroll
-      for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
-        const bool busy = lng && lds_ld_sync(ra + 12u) != 0u;
-        if (ballot(busy) == 0u) break;
-        lk_sleep();
-      }
-      if (lng) {
-        lds_st_sync(ra, static_cast<uint32_t>(na));
-        lds_st_sync(ra + 4u, static_cast<uint32_t>(na >> 32));
-        lds_st_sync(ra + 8u, nb);
-      }
-      lgkm_wait();  // the record before its marker
-      if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(s) + 1u);
+    for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
+      const bool busy = lng && lds_ld_sync(ra + 12u) != 0u;
+      if (ballot(busy) == 0u) break;
+      lk_sleep();
     }
-    lgkm_wait();  // queued before the in-flight count drops
-    if (l == 0u) lds_add(MiscAddr(kMiscDesks), 0xffffffffu);
-    npub = true;
+    if (lng) {
+      lds_st_sync(ra, static_cast<uint32_t>(a));
+      lds_st_sync(ra + 4u, static_cast<uint32_t>(a >> 32));
+      lds_st_sync(ra + 8u, b);
+    }
+    lgkm_wait();  // the record before its marker
+    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(base + l) + 1u);
+    if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0u - k);  // (after the records: in order)
   };
-  // The next desk becomes the desk (its short spans for the ring).
+
+  // The next desk, once its descriptors are in: its empty spans answered,
+  // its short and long spans sorted into lane masks (the long ones held by
+  // this wave, counted in the workgroup's held count before the desk leaves
+  // the in-flight count).
+  auto sort_desk = [&]() {
+    const bool live = l < 16u && ((nlive >> (l & 15u)) & 1u) != 0u;
+    const uint64_t s = nbase + l;
+    const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
+    const bool empty = live && p.empty;
+    if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
+    nshort = static_cast<uint32_t>(ballot(live && !p.empty && p.m == 0u));
+    nlong = static_cast<uint32_t>(ballot(live && !p.empty && p.m != 0u));
+    if (l == 0u) {
+      if (nlong != 0u) lds_add(MiscAddr(kMiscHeld), static_cast<uint32_t>(__builtin_popcount(nlong)));
+      lds_add(MiscAddr(kMiscDesks), 0xffffffffu);
+    }
+    nsorted = true;
+  };
+  // Waves out of work (the idle count): this wave's held long spans, of the
+  // desk and of the sorted next desk, into the queue.
+  auto share = [&]() {
+    if (dlong != 0u) queue_longs(dlong, da, dn, dbase);
+    if (nstate == 2u && nsorted && nlong != 0u) queue_longs(nlong, na, src.bytes(nn), nbase);
+    dlong = 0;
+    nlong = 0;
+  };
+  // The desk's next own long span becomes the prefetched one.
+  auto take_own = [&]() {
+    const uint32_t k = static_cast<uint32_t>(__builtin_ctz(dlong));
+    pfa = (static_cast<uint64_t>(rdlane(static_cast<uint32_t>(da >> 32), k)) << 32) |
+          rdlane(static_cast<uint32_t>(da), k);
+    pfn = rdlane(dn, k);
+    pfinit = rdlane(di, k);
+    pfid = static_cast<uint32_t>(dbase) + k;
+    pfvalid = true;
+    dlong &= dlong - 1u;
+    if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0xffffffffu);
+  };
+  // The next desk becomes the desk.
   auto switch_desk = [&]() {
-    if (!npub) publish_desk();
+    if (!nsorted) sort_desk();
     da = na;
     dn = src.bytes(nn);
     di = ni;
     dbase = nbase;
     dshort = nshort;
+    dlong = nlong;
+    nlong = 0;
     nstate = 0;
   };
 
@@ -444,7 +472,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         push_shorts();
         continue;
       }
-      pop();
+      if (dlong != 0u) {
+        take_own();
+        continue;
+      }
+      pop();  // long spans another wave shared
       loads_landed(pfinit);
       if (pfvalid) continue;
       if (nstate != 0u) {
@@ -460,26 +492,30 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         loads_landed(ni);
         continue;
       }
-      // nothing of this wave's own: a desk another wave grabbed may still
-      // queue long spans -- wait for it (bounded) rather than leave them to
-      // that wave alone
+      // out of work: counted idle, so that the waves holding long spans
+      // share them, take what they queue until none is held and no desk is
+      // in flight (bounded)
+      if (l == 0u) lds_add(MiscAddr(kMiscIdle), 1u);
       bool again = false;
 #pragma nounroll
       for (uint32_t spin = 0; spin < (1u << 16); ++spin) {
-        if (uni(lds_ld_sync(MiscAddr(kMiscDesks))) == 0u) {
-          pop();
-          loads_landed(pfinit);
-          again = pfvalid;
-          break;
-        }
-        lk_sleep();
         pop();
-        loads_landed(pfinit);
         if (pfvalid) {
           again = true;
           break;
         }
+        const uint32_t held = uni(lds_ld_sync(MiscAddr(kMiscHeld)));
+        const uint32_t desks = uni(lds_ld_sync(MiscAddr(kMiscDesks)));
+        lgkm_wait();  // (both read before the queue is looked at again)
+        if (held == 0u && desks == 0u) {
+          pop();
+          again = pfvalid;
+          break;
+        }
+        lk_sleep();
       }
+      if (l == 0u) lds_add(MiscAddr(kMiscIdle), 0xffffffffu);
+      loads_landed(pfinit);
       if (!again) break;
     }
     if (rcnt != 0u) issue_batch();
@@ -499,6 +535,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   for (;;) {
     LP_T(t0);
     uint32_t W[16];
+    uint32_t idle = 0;  // waves of the workgroup out of work
     u32x4 ax{0, 0, 0, 0};
     if (have) {
       if (stored_prev) wait_vm<1>();
@@ -512,9 +549,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       cb_id = nb_id;
       cb_j = nb_j;
       csplit = nsplit;
+      const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));  // (rides with the slot's reads)
       pp.read(W);
       if (ckind == kWSeg && (cs.fl & kSAux)) ax = lds_ld4(SegAuxAddr(w));
       pp.release();
+      idle = uni(idle_w);
     } else {
       ckind = kWNone;
     }
@@ -647,8 +686,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       // while the DMA flies: queue the next desk's long spans once it is in,
       // and take the next long span when this one is about to end (not
       // earlier: another wave may be idle)
-      if (nstate == 2u && !npub) publish_desk();
-      if (!pfvalid && (!lvalid || lt + 1u >= lsp.m)) pop();
+      if (nstate == 2u && !nsorted) sort_desk();
+      if (!pfvalid && (!lvalid || lt + 1u >= lsp.m)) {
+        if (dlong != 0u) take_own();
+        else pop();
+      }
+      if (idle != 0u && (dlong | nlong) != 0u) share();
     }
     // the next desk's descriptor loads go out after this iteration's DMA and
     // store: the wait for that DMA covers them (nothing in decide waits on
