@@ -92,6 +92,8 @@ def cpu_rates(host, offs, lens):
     """BASELINE config 3's CPU side: the library's host CRC path (SSE4.2
     3-stream + PCLMUL combine, the reference's crc32c_3way class) over the
     same spans from host memory, 1 thread and all usable CPUs, GiB/s."""
+    if NO_CPU:
+        return [None, None]
     nbytes = float(lens.sum())
     out = []
     for threads in (1, usable_cpus()):
@@ -110,6 +112,7 @@ def check_sample(host, offs, lens, got, rng, k=4000):
 
 SPLIT = False  # --split: HCRC_SPLIT_SMALL on the device batches
 SPLIT_LONG = False  # --split-long: HCRC_SPLIT_LONG on config 3's device batches
+NO_CPU = False  # --no-cpu: skip the CPU rates (same-session A/B runs)
 
 
 def batch_latency(eng, dbuf, do, dl, stream, nbatch_bytes=2 << 20, reps=200):
@@ -321,12 +324,14 @@ def main():
     ap.add_argument("--split", action="store_true", help="HCRC_SPLIT_SMALL on device batches")
     ap.add_argument("--split-long", action="store_true",
                     help="HCRC_SPLIT_LONG on config 3's device batches")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU rates of config 3")
     ap.add_argument("--mixed-gib", type=float, default=2.0)
     ap.add_argument("--ssts", type=int, default=256)
     ap.add_argument("--host-blocks", type=int, default=1 << 18)
     a = ap.parse_args()
-    global SPLIT, SPLIT_LONG
+    global SPLIT, SPLIT_LONG, NO_CPU
     SPLIT = a.split
+    NO_CPU = a.no_cpu
     SPLIT_LONG = a.split_long
     rng = np.random.default_rng(42)
     d = torch.device("cuda", 0)

@@ -12,13 +12,14 @@ WHAT=$2
 shift 2
 for r in $(seq 1 "$ROUNDS"); do
   for v in "$@"; do
+    tag=$(basename "$v" .so)
     if [ "$v" = tree ]; then unset WIPDB_HCRC_LIB; else export WIPDB_HCRC_LIB=$PWD/$v; fi
     timeout -k 10 120 python bench.py --no-cpu-baseline --steps 50 > gpurun_out/ab_bench.log 2>&1 || exit $?
     b=$(grep -o '"kernel_avg_ms": [0-9.]*\|"mismatches": [0-9]*' gpurun_out/ab_bench.log | tr '\n' ' ')
     e=""
     if [ -n "$WHAT" ] && [ "$WHAT" != none ]; then
-      timeout -k 10 200 python scripts/bench_extra.py --what "$WHAT" > gpurun_out/ab_extra.log 2>&1 || exit $?
-      e=$(grep -o '"ms": [0-9.]*\|"kernel_ms": [0-9.]*\|"GiBps_end_to_end": [0-9.]*' gpurun_out/ab_extra.log | tr '\n' ' ')
+      timeout -k 10 300 python scripts/bench_extra.py --no-cpu --what "$WHAT" > gpurun_out/ab_extra_${r}_${tag}.log 2>&1 || exit $?
+      e=$(grep -o '"GiBps": [0-9.]*\|"GiBps_end_to_end": [0-9.]*' gpurun_out/ab_extra_${r}_${tag}.log | tr '\n' ' ')
     fi
     echo "round $r $v: headline $b | $e"
   done

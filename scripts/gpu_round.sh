@@ -30,7 +30,7 @@ for s in $STEPS; do
     extra) run extra 400 python scripts/bench_extra.py --what mixed,tblocks,vtblocks,verify ;;
     mixed) run mixed 300 python scripts/bench_extra.py --what mixed ;;
     host) run host 400 python scripts/bench_extra.py --what sst,host4k ;;
-    ab) run ab 600 bash scripts/gpu_abn.sh 2 tblocks,vtblocks,verify tree build/ab/lib_r02.so ;;
+    ab) run ab 900 bash scripts/gpu_abn.sh ${AB_ROUNDS:-2} ${AB_WHAT:-mixed,tblocks,vtblocks,verify} tree ${AB_LIBS:-build/ab/lib_r02.so} ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${P}_pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${P}_pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
