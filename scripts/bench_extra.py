@@ -11,6 +11,8 @@ PCIe-inclusive host path) -- one JSON line each, for DESIGN.md.
              filter block, one metaindex block) in HOST memory, checksummed
              through hcrc_batch(HOST_PTRS): pinned staging + H2D + kernel +
              D2H, overlapped -- the PCIe-inclusive end-to-end rate.
+  sstpin     config 5 from PINNED host memory (the table builder's write
+             buffers): zero-copy, as a fraction of the measured PCIe ceiling.
   host4k     the headline 1 M x 4 KiB blocks from host memory (PCIe-inclusive).
 
 Every batch is checked against the library's host CPU path on a sample.
@@ -304,6 +306,57 @@ def run_sst(eng, rng, n_sst):
             "mismatches_in_sample": int((want != got[idx]).sum())}
 
 
+def pcie_h2d_ceiling(nbytes=1 << 30, reps=5):
+    """The measured PCIe host-to-device ceiling: a pinned (torch
+    pin_memory) -> HBM copy of nbytes by the copy engine, GiB/s."""
+    src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    del src, dst
+    return round(nbytes / t / 2**30, 2)
+
+
+def run_sst_pinned(eng, rng, n_sst):
+    """Config 5 through the product path the table layer takes: the SST
+    stream in pinned host memory (hcrc_host_alloc -- TableBuilder's pooled
+    write buffers are such memory), hcrc_batch(HOST_PTRS) finds every span
+    in it and runs zero-copy (the kernel reads the spans over PCIe), as a
+    fraction of the measured PCIe H2D ceiling."""
+    import ctypes
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    offs, lens, nbytes = sst_layout(rng, n_sst)
+    pin = ctypes.c_void_p()
+    _lib.check(lib.hcrc_host_alloc(nbytes, ctypes.byref(pin)), "hcrc_host_alloc")
+    try:
+        host = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(pin.value))
+        host[:] = rng.integers(32, 127, nbytes, dtype=np.uint8)
+        eng.batch(host, offs[:1000], lens[:1000])
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = eng.batch(host, offs, lens, mask_output=True)
+        t = (time.perf_counter() - t0) / reps
+        idx = rng.choice(offs.size, 4000, replace=False)
+        want = cpu_batch(host, offs[idx], lens[idx], mask_output=True)
+        ceiling = pcie_h2d_ceiling()
+        rate = float(lens.sum()) / t / 2**30
+        return {"config": "5 8Binsert SST stream in PINNED host memory (TableBuilder's write "
+                          "buffers), hcrc_batch HOST_PTRS -> zero-copy, PCIe-inclusive",
+                "ssts": n_sst, "spans": int(offs.size), "bytes": int(lens.sum()),
+                "GiBps_end_to_end": round(rate, 2), "pcie_h2d_ceiling_GiBps": ceiling,
+                "fraction_of_pcie_ceiling": round(rate / ceiling, 3),
+                "mismatches_in_sample": int((want != got[idx]).sum())}
+    finally:
+        lib.hcrc_host_free(pin)
+
+
 def run_host4k(eng, rng, nblk):
     host = rng.integers(0, 256, nblk * 4096, dtype=np.uint8)
     offs = np.arange(nblk, dtype=np.uint64) * 4096
@@ -348,6 +401,8 @@ def main():
                 r = run_vtblocks(eng, d, stream, rng)
             elif w == "sst":
                 r = run_sst(eng, rng, a.ssts)
+            elif w == "sstpin":
+                r = run_sst_pinned(eng, rng, a.ssts)
             elif w == "host4k":
                 r = run_host4k(eng, rng, a.host_blocks)
             else:

@@ -174,6 +174,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // ---- the desk (lanes 0..15) and the next desk, loading ----
   uint64_t da = 0, na = 0;
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
+  uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words (switch_desk)
   uint64_t dbase = 0, nbase = 0;
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
   uint32_t dlong = 0;         // desk lanes whose long span this wave has not taken
@@ -183,11 +184,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   bool nsorted = false;       // next desk: sorted (empty spans answered)
   bool exhausted = false;
   // ---- the long span being run, and the next one (taken from the queue) ----
-  Plan lsp{};
+  // (c0 = a - hp, plan word, piece word: crc32c_plan.h PackPL)
+  uint64_t lc0 = 0;
+  uint32_t lpl = 0, lpw = 0;
   uint32_t lt = 0, linit = 0, lid = 0;
   bool lvalid = false;
   uint64_t pfa = 0;
-  uint32_t pfn = 0, pfid = 0, pfinit = 0;
+  uint32_t pfpl = 0, pfpw = 0, pfid = 0, pfinit = 0;
   bool pfvalid = false;
   // ---- the iterations: current and next ----
   uint32_t ckind = kWNone, nkind = kWNone, cused = 0, nused = 0;
@@ -256,9 +259,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (l == 0u) lds_st_sync(ra + 12u, 0u);
     if (r3 == 0u) return;  // never written (cannot happen; no hang if it does)
     pfa = (static_cast<uint64_t>(r1) << 32) | r0;
-    pfn = r2;
     pfid = r3 - 1u;
     pfinit = src.init_of(pfid);  // (0 without an init column; the strided blocks' init)
+    const Plan p = MakePlan(pfa, static_cast<uint32_t>(sbase + pfa), r2, kV);
+    pfpl = PackPL(p);
+    pfpw = p.pw;
     pfvalid = true;
   };
   // The long spans of desk lanes m (a, bytes b, span base + lane) into the
@@ -319,7 +324,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t k = static_cast<uint32_t>(__builtin_ctz(dlong));
     pfa = (static_cast<uint64_t>(rdlane(static_cast<uint32_t>(da >> 32), k)) << 32) |
           rdlane(static_cast<uint32_t>(da), k);
-    pfn = rdlane(dn, k);
+    pfpl = rdlane(dpl, k);
+    pfpw = rdlane(dpw, k);
     pfinit = rdlane(di, k);
     pfid = static_cast<uint32_t>(dbase) + k;
     pfvalid = true;
@@ -329,6 +335,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // The next desk becomes the desk.
   auto switch_desk = [&]() {
     if (!nsorted) sort_desk();
+    {
+      const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
+      dpl = PackPL(p);
+      dpw = p.pw;
+    }
     da = na;
     dn = src.bytes(nn);
     di = ni;
@@ -344,13 +355,14 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t room = 64u - rcnt;
     const uint32_t c = static_cast<uint32_t>(__builtin_popcount(dshort));
     const uint32_t take = c < room ? c : room;
-    // desk lane l: its piece (valid in the short lanes)
-    const Plan p = MakePlan(da, static_cast<uint32_t>(sbase + da), dn, kV);
-    const uint32_t inj = head_register_lane(l, di, p.hp);
+    // desk lane l: its piece (valid in the short lanes: the whole span, m = 0)
+    const uint32_t hp = PL_hp(dpl);
+    const uint64_t p0 = da - hp;
+    const uint32_t inj = head_register_lane(l, di, hp);
     const uint32_t rank = mbcnt_lo(dshort, 0u);
     const bool tk = l < 16u && ((dshort >> (l & 15u)) & 1u) != 0u && rank < take;
     const uint32_t tmask = static_cast<uint32_t>(ballot(tk));
-    const uint32_t nl_sum = scan_add(tk ? PW{p.pw}.nl() : 0u, l);
+    const uint32_t nl_sum = scan_add(tk ? PW{dpw}.nl() : 0u, l);
     // ring lane q in [rcnt, rcnt + take) pulls the (q - rcnt)-th short lane
     const uint32_t kq = l - rcnt;
     uint32_t pos = 0;
@@ -360,9 +372,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       pos = static_cast<uint32_t>(__builtin_popcount(below)) <= kq ? pos + st : pos;
     }
     const bool me = l >= rcnt && kq < take;
-    const uint32_t v_lo = bperm(static_cast<uint32_t>(p.p0), pos);
-    const uint32_t v_hi = bperm(static_cast<uint32_t>(p.p0 >> 32), pos);
-    const uint32_t v_pw = bperm(p.pw, pos), v_inj = bperm(inj, pos);
+    const uint32_t v_lo = bperm(static_cast<uint32_t>(p0), pos);
+    const uint32_t v_hi = bperm(static_cast<uint32_t>(p0 >> 32), pos);
+    const uint32_t v_pw = bperm(dpw, pos), v_inj = bperm(inj, pos);
     const uint32_t v_id = static_cast<uint32_t>(dbase) + pos;
     rp_lo = me ? v_lo : rp_lo;
     rp_hi = me ? v_hi : rp_hi;
@@ -376,20 +388,24 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
 
   // ---- decide: issue the next iteration's DMA ----
   auto issue_seg = [&]() {
-    const uint64_t wb = sbase + lsp.c0 + 4096u * static_cast<uint64_t>(lt);
+    const uint32_t m = PL_m(lpl);
+    const uint64_t p0 = lc0 + 4096u * static_cast<uint64_t>(m);  // the back piece / span grid end
+    const uint64_t wb = sbase + lc0 + 4096u * static_cast<uint64_t>(lt);
     const uint32_t o = 16u * pp.cm;
-    const uint32_t s0 = lt == 0u ? 4u * lsp.ws : 0u;
+    const uint32_t s0 = lt == 0u ? 4u * PL_ws(lpl) : 0u;
     dma4(wb, pp.slot, o > s0 ? o : s0, o + 1024u, o + 2048u, o + 3072u);
-    const bool last = lt + 1u == lsp.m;
+    const bool last = lt + 1u == m;
+    const bool aux = last && PL_aux(lpl) != 0u;
     ns.fl = (lt == 0u ? kSFirst : 0u) | (last ? kSLast : 0u) |
-            (last && lsp.pw != 0u ? kSPush : 0u) | (last && lsp.seg_aux ? kSAux : 0u);
-    if (last && lsp.seg_aux)
-      dma_piece(l, sbase + lsp.c0 + 16u * static_cast<uint64_t>(lsp.C) - 12u, 0u, SegAuxAddr(w));
-    ns.hw = lsp.hp | (lsp.ws << 4) | (lsp.k << 6) | (lsp.jv << 8);
+            (last && lpw != 0u ? kSPush : 0u) | (aux ? kSAux : 0u);
+    // (seg_aux: no piece, so the grid ends at c0 + 4096 m; the aux chunk is
+    // the 16 bytes ending at E4 + 4)
+    if (aux) dma_piece(l, sbase + p0 - 12u, 0u, SegAuxAddr(w));
+    ns.hw = PL_hw(lpl);
     ns.init = linit;
     ns.id = lid;
-    ns.pw = lsp.pw;
-    ns.p0 = lsp.p0;
+    ns.pw = lpw;
+    ns.p0 = p0;
     nkind = kWSeg;
     ++lt;
     if (last) lvalid = false;
@@ -451,7 +467,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     rlanes -= used;
   };
   auto start_long = [&]() {
-    lsp = MakePlan(pfa, static_cast<uint32_t>(sbase + pfa), pfn, kV);
+    lc0 = pfa - PL_hp(pfpl);
+    lpl = pfpl;
+    lpw = pfpw;
     lt = 0;
     linit = pfinit;
     lid = pfid;
@@ -687,7 +705,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       // and take the next long span when this one is about to end (not
       // earlier: another wave may be idle)
       if (nstate == 2u && !nsorted) sort_desk();
-      if (!pfvalid && (!lvalid || lt + 1u >= lsp.m)) {
+      if (!pfvalid && (!lvalid || lt + 1u >= PL_m(lpl))) {
         if (dlong != 0u) take_own();
         else pop();
       }

@@ -162,6 +162,19 @@ WIPDB_LK_HD inline Plan MakePlan(uint64_t a, uint32_t s_lo, uint32_t n, bool ver
   return p;
 }
 
+// ---- plan word: what a wave needs of a span with segments besides its
+// address (c0 = a - hp) and piece word, packed so a desk lane hands it over
+// in one readlane:  hp (4) | ws (2) << 4 | k (2) << 6 | jv (2) << 8 |
+// seg_aux << 10 | m << 11  (the low 10 bits are a segment's `hw`).
+WIPDB_LK_HD inline uint32_t PackPL(const Plan& p) {
+  return p.hp | (p.ws << 4) | (p.k << 6) | (p.jv << 8) | (p.seg_aux << 10) | (p.m << 11);
+}
+WIPDB_LK_HD inline uint32_t PL_hp(uint32_t pl) { return pl & 15u; }
+WIPDB_LK_HD inline uint32_t PL_ws(uint32_t pl) { return (pl >> 4) & 3u; }
+WIPDB_LK_HD inline uint32_t PL_hw(uint32_t pl) { return pl & 1023u; }
+WIPDB_LK_HD inline uint32_t PL_aux(uint32_t pl) { return (pl >> 10) & 1u; }
+WIPDB_LK_HD inline uint32_t PL_m(uint32_t pl) { return pl >> 11; }
+
 // ---- the batch window of a piece (lanes j = 0 .. nl - 1 of its group) ----
 // Window chunk w (0 .. 4 nl - 1) of the piece with first real chunk at p0:
 // w > front reads p0 + 16 (w - front); w == front, its first real chunk,
