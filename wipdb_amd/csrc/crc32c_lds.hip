@@ -38,12 +38,6 @@
 
 #include "crc32c_dev.h"
 
-// Desks of spans strided over the batch (see grab_desk); 0: 16 consecutive
-// spans per desk (an A/B build)
-#ifndef WIPDB_LP_STRIDED_DESKS
-#define WIPDB_LP_STRIDED_DESKS 1
-#endif
-
 namespace wipdb {
 namespace lk {
 
@@ -182,7 +176,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
   uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words (switch_desk)
   uint64_t dbase = 0, nbase = 0;
-  uint32_t dstride = 1, nstride = 1;  // desk lane j is span base + j * stride
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
   uint32_t dlong = 0;         // desk lanes whose long span this wave has not taken
   uint32_t nlive = 0;         // next desk: lanes holding a span
@@ -214,36 +207,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     uint32_t u = 0;
     if (l == 0u) u = lds_add(MiscAddr(kMiscUnit), 16u);
     u = uni(u);
-    // desk D of the launch (the workgroup's desks are D = g, g + grid, ...)
-    const uint32_t D = (u >> 4) * group_count() + group_id();
-#if WIPDB_LP_STRIDED_DESKS
-    // Rounds of K = 16 * grid desks cover 16 K spans: desk q of a round holds
-    // spans q, q + K, q + 2 K, ... (q + 15 K) -- the desks in flight at once
-    // (about one per wave) read neighbouring spans at the same time, so the
-    // chip streams one compact window of the batch (DRAM rows opened once),
-    // not one window per desk.  The last round strides by ceil(rem / 16).
-    const uint32_t K = 16u * group_count();
-    const uint32_t r = D / K, q = D - r * K;
-    const uint64_t r0 = static_cast<uint64_t>(r) * 16u * K;
-    const uint64_t rem = r0 < count ? count - r0 : 0u;
-    const uint32_t Kr = rem >= 16u * static_cast<uint64_t>(K) ? K : static_cast<uint32_t>((rem + 15u) >> 4);
-    if (q >= Kr) {
-      exhausted = true;
-      nstate = 0;
-      return;
-    }
-    nbase = r0 + q;
-    nstride = Kr;
-#else
-    nbase = static_cast<uint64_t>(D) * 16u;
-    nstride = 1;
+    nbase = (static_cast<uint64_t>(u >> 4) * group_count() + group_id()) * 16u;
     if (nbase >= count) {
       exhausted = true;
       nstate = 0;
       return;
     }
-#endif
-    const uint64_t s = nbase + static_cast<uint64_t>(l) * nstride;
+    const uint64_t s = nbase + l;
     const bool v = l < 16u && s < count;
     nlive = static_cast<uint32_t>(ballot(v));
     if (v) src.lane(s, na, nn, ni);
@@ -298,7 +268,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   };
   // The long spans of desk lanes m (a, bytes b, span base + lane) into the
   // queue; they leave the workgroup's held count once queued.
-  auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint64_t base, uint32_t stride) {
+  auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint64_t base) {
     const bool lng = l < 16u && ((m >> (l & 15u)) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
     const uint32_t k = static_cast<uint32_t>(__builtin_popcount(m));
     uint32_t q = 0;
@@ -319,7 +289,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       lds_st_sync(ra + 8u, b);
     }
     lgkm_wait();  // the record before its marker
-    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(base + static_cast<uint64_t>(l) * stride) + 1u);
+    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(base + l) + 1u);
     if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0u - k);  // (after the records: in order)
   };
 
@@ -329,7 +299,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // the in-flight count).
   auto sort_desk = [&]() {
     const bool live = l < 16u && ((nlive >> (l & 15u)) & 1u) != 0u;
-    const uint64_t s = nbase + static_cast<uint64_t>(l) * nstride;
+    const uint64_t s = nbase + l;
     const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
     const bool empty = live && p.empty;
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
@@ -344,8 +314,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // Waves out of work (the idle count): this wave's held long spans, of the
   // desk and of the sorted next desk, into the queue.
   auto share = [&]() {
-    if (dlong != 0u) queue_longs(dlong, da, dn, dbase, dstride);
-    if (nstate == 2u && nsorted && nlong != 0u) queue_longs(nlong, na, src.bytes(nn), nbase, nstride);
+    if (dlong != 0u) queue_longs(dlong, da, dn, dbase);
+    if (nstate == 2u && nsorted && nlong != 0u) queue_longs(nlong, na, src.bytes(nn), nbase);
     dlong = 0;
     nlong = 0;
   };
@@ -357,7 +327,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     pfpl = rdlane(dpl, k);
     pfpw = rdlane(dpw, k);
     pfinit = rdlane(di, k);
-    pfid = static_cast<uint32_t>(dbase) + k * dstride;
+    pfid = static_cast<uint32_t>(dbase) + k;
     pfvalid = true;
     dlong &= dlong - 1u;
     if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0xffffffffu);
@@ -374,7 +344,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     dn = src.bytes(nn);
     di = ni;
     dbase = nbase;
-    dstride = nstride;
     dshort = nshort;
     dlong = nlong;
     nlong = 0;
@@ -406,7 +375,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t v_lo = bperm(static_cast<uint32_t>(p0), pos);
     const uint32_t v_hi = bperm(static_cast<uint32_t>(p0 >> 32), pos);
     const uint32_t v_pw = bperm(dpw, pos), v_inj = bperm(inj, pos);
-    const uint32_t v_id = static_cast<uint32_t>(dbase) + pos * dstride;
+    const uint32_t v_id = static_cast<uint32_t>(dbase) + pos;
     rp_lo = me ? v_lo : rp_lo;
     rp_hi = me ? v_hi : rp_hi;
     rpw = me ? v_pw : rpw;
