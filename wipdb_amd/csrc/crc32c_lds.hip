@@ -175,7 +175,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint64_t da = 0, na = 0;
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
   uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words (switch_desk)
-  uint64_t dbase = 0, nbase = 0;
+  uint32_t dbase = 0, nbase = 0;  // (a launch holds < 2^31 spans)
+  uint32_t dtotal = 0;        // the desk's long spans still counted in the held count
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
   uint32_t dlong = 0;         // desk lanes whose long span this wave has not taken
   uint32_t nlive = 0;         // next desk: lanes holding a span
@@ -183,21 +184,19 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t nstate = 0;        // next desk: 0 none, 1 loads issued, 2 loads waited for
   bool nsorted = false;       // next desk: sorted (empty spans answered)
   bool exhausted = false;
-  // ---- the long span being run, and the next one (taken from the queue) ----
+  // ---- the long span being run (taken from the desk or the queue) ----
   // (c0 = a - hp, plan word, piece word: crc32c_plan.h PackPL)
   uint64_t lc0 = 0;
   uint32_t lpl = 0, lpw = 0;
   uint32_t lt = 0, linit = 0, lid = 0;
   bool lvalid = false;
-  uint64_t pfa = 0;
-  uint32_t pfpl = 0, pfpw = 0, pfid = 0, pfinit = 0;
-  bool pfvalid = false;
   // ---- the iterations: current and next ----
-  uint32_t ckind = kWNone, nkind = kWNone, cused = 0, nused = 0;
+  // kind (2) | a batch's lanes (7) << 2 | its split piece's first lane
+  // (7; 64: none) << 9
+  uint32_t ck = kWNone, nk = kWNone;
   SegW cs{}, ns{};
   uint32_t cb_pw = 0, cb_inj = 0, cb_id = 0, cb_j = 0;  // batch, per lane
   uint32_t nb_pw = 0, nb_inj = 0, nb_id = 0, nb_j = 0;
-  uint32_t csplit = 64, nsplit = 64;  // a batch's split piece: its first lane (64: none)
   uint32_t carry = 0, carry_tw = 0;   // the split piece's register over its first lanes, tail word
   uint32_t chain = 0;
 
@@ -207,13 +206,14 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     uint32_t u = 0;
     if (l == 0u) u = lds_add(MiscAddr(kMiscUnit), 16u);
     u = uni(u);
-    nbase = (static_cast<uint64_t>(u >> 4) * group_count() + group_id()) * 16u;
-    if (nbase >= count) {
+    const uint64_t nb64 = (static_cast<uint64_t>(u >> 4) * group_count() + group_id()) * 16u;
+    nbase = static_cast<uint32_t>(nb64);
+    if (nb64 >= count) {
       exhausted = true;
       nstate = 0;
       return;
     }
-    const uint64_t s = nbase + l;
+    const uint64_t s = nb64 + l;
     const bool v = l < 16u && s < count;
     nlive = static_cast<uint32_t>(ballot(v));
     if (v) src.lane(s, na, nn, ni);
@@ -258,17 +258,21 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     lgkm_wait();  // read before the slot is freed
     if (l == 0u) lds_st_sync(ra + 12u, 0u);
     if (r3 == 0u) return;  // never written (cannot happen; no hang if it does)
-    pfa = (static_cast<uint64_t>(r1) << 32) | r0;
-    pfid = r3 - 1u;
-    pfinit = src.init_of(pfid);  // (0 without an init column; the strided blocks' init)
-    const Plan p = MakePlan(pfa, static_cast<uint32_t>(sbase + pfa), r2, kV);
-    pfpl = PackPL(p);
-    pfpw = p.pw;
-    pfvalid = true;
+    const uint64_t a = (static_cast<uint64_t>(r1) << 32) | r0;
+    lid = r3 - 1u;
+    // (0 without an init column; the strided blocks' init.  A stall on the
+    // load: shared spans are rare)
+    linit = uni(src.init_of(lid));
+    const Plan p = MakePlan(a, static_cast<uint32_t>(sbase + a), r2, kV);
+    lpl = PackPL(p);
+    lpw = p.pw;
+    lc0 = p.c0;
+    lt = 0;
+    lvalid = true;
   };
   // The long spans of desk lanes m (a, bytes b, span base + lane) into the
   // queue; they leave the workgroup's held count once queued.
-  auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint64_t base) {
+  auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint32_t base, uint32_t held) {
     const bool lng = l < 16u && ((m >> (l & 15u)) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
     const uint32_t k = static_cast<uint32_t>(__builtin_popcount(m));
     uint32_t q = 0;
@@ -289,8 +293,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       lds_st_sync(ra + 8u, b);
     }
     lgkm_wait();  // the record before its marker
-    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(base + l) + 1u);
-    if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0u - k);  // (after the records: in order)
+    if (lng) lds_st_sync(ra + 12u, base + l + 1u);
+    if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0u - held);  // (after the records: in order)
   };
 
   // The next desk, once its descriptors are in: its empty spans answered,
@@ -299,7 +303,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // the in-flight count).
   auto sort_desk = [&]() {
     const bool live = l < 16u && ((nlive >> (l & 15u)) & 1u) != 0u;
-    const uint64_t s = nbase + l;
+    const uint64_t s = static_cast<uint64_t>(nbase) + l;
     const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
     const bool empty = live && p.empty;
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
@@ -313,24 +317,34 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   };
   // Waves out of work (the idle count): this wave's held long spans, of the
   // desk and of the sorted next desk, into the queue.
+  // (the desk's long spans leave the held count all at once: those it has
+  // taken and those it queues now)
   auto share = [&]() {
-    if (dlong != 0u) queue_longs(dlong, da, dn, dbase);
-    if (nstate == 2u && nsorted && nlong != 0u) queue_longs(nlong, na, src.bytes(nn), nbase);
+    if (dlong != 0u) queue_longs(dlong, da, dn, dbase, dtotal);
+    if (nstate == 2u && nsorted && nlong != 0u)
+      queue_longs(nlong, na, src.bytes(nn), nbase, static_cast<uint32_t>(__builtin_popcount(nlong)));
     dlong = 0;
+    dtotal = 0;
     nlong = 0;
   };
-  // The desk's next own long span becomes the prefetched one.
+  // The desk's next own long span becomes the one being run; the desk's
+  // long spans leave the held count when the last is taken.
   auto take_own = [&]() {
     const uint32_t k = static_cast<uint32_t>(__builtin_ctz(dlong));
-    pfa = (static_cast<uint64_t>(rdlane(static_cast<uint32_t>(da >> 32), k)) << 32) |
-          rdlane(static_cast<uint32_t>(da), k);
-    pfpl = rdlane(dpl, k);
-    pfpw = rdlane(dpw, k);
-    pfinit = rdlane(di, k);
-    pfid = static_cast<uint32_t>(dbase) + k;
-    pfvalid = true;
+    const uint32_t pl = rdlane(dpl, k);
+    lc0 = ((static_cast<uint64_t>(rdlane(static_cast<uint32_t>(da >> 32), k)) << 32) |
+           rdlane(static_cast<uint32_t>(da), k)) - PL_hp(pl);
+    lpl = pl;
+    lpw = rdlane(dpw, k);
+    linit = rdlane(di, k);
+    lid = dbase + k;
+    lt = 0;
+    lvalid = true;
     dlong &= dlong - 1u;
-    if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0xffffffffu);
+    if (dlong == 0u) {
+      if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0u - dtotal);
+      dtotal = 0;
+    }
   };
   // The next desk becomes the desk.
   auto switch_desk = [&]() {
@@ -346,6 +360,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     dbase = nbase;
     dshort = nshort;
     dlong = nlong;
+    dtotal = static_cast<uint32_t>(__builtin_popcount(nlong));
     nlong = 0;
     nstate = 0;
   };
@@ -375,7 +390,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t v_lo = bperm(static_cast<uint32_t>(p0), pos);
     const uint32_t v_hi = bperm(static_cast<uint32_t>(p0 >> 32), pos);
     const uint32_t v_pw = bperm(dpw, pos), v_inj = bperm(inj, pos);
-    const uint32_t v_id = static_cast<uint32_t>(dbase) + pos;
+    const uint32_t v_id = dbase + pos;
     rp_lo = me ? v_lo : rp_lo;
     rp_hi = me ? v_hi : rp_hi;
     rpw = me ? v_pw : rpw;
@@ -406,7 +421,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     ns.id = lid;
     ns.pw = lpw;
     ns.p0 = p0;
-    nkind = kWSeg;
+    nk = kWSeg;
     ++lt;
     if (last) lvalid = false;
   };
@@ -453,9 +468,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     nb_inj = b_inj;
     nb_id = b_id;
     nb_j = j;
-    nused = used;
-    nsplit = part ? usedf : 64u;
-    nkind = kWBatch;
+    nk = kWBatch | (used << 2) | ((part ? usedf : 64u) << 9);
     // the ring drops its first n entries; a split one stays at its head
     rp_lo = bperm(rp_lo, l + n);
     rp_hi = bperm(rp_hi, l + n);
@@ -466,22 +479,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     rcnt -= n;
     rlanes -= used;
   };
-  auto start_long = [&]() {
-    lc0 = pfa - PL_hp(pfpl);
-    lpl = pfpl;
-    lpw = pfpw;
-    lt = 0;
-    linit = pfinit;
-    lid = pfid;
-    lvalid = true;
-    pfvalid = false;
-  };
   // Chooses and issues the next iteration (nkind = kWNone: no work left).
   auto decide = [&]() {
-    nkind = kWNone;
+    nk = kWNone;
     for (int guard = 0; guard < 64; ++guard) {
       if (rcnt != 0u && (rlanes >= 64u || rcnt == 64u)) break;  // a full batch
-      if (!lvalid && pfvalid) start_long();
       if (lvalid) {
         issue_seg();
         return;
@@ -495,8 +497,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         continue;
       }
       pop();  // long spans another wave shared
-      loads_landed(pfinit);
-      if (pfvalid) continue;
+      if (lvalid) continue;
       if (nstate != 0u) {
         // (stalls on the desk's loads if they were issued just now)
         switch_desk();
@@ -518,7 +519,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
 #pragma nounroll
       for (uint32_t spin = 0; spin < (1u << 16); ++spin) {
         pop();
-        if (pfvalid) {
+        if (lvalid) {
           again = true;
           break;
         }
@@ -527,13 +528,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         lgkm_wait();  // (both read before the queue is looked at again)
         if (held == 0u && desks == 0u) {
           pop();
-          again = pfvalid;
+          again = lvalid;
           break;
         }
         lk_sleep();
       }
       if (l == 0u) lds_add(MiscAddr(kMiscIdle), 0xffffffffu);
-      loads_landed(pfinit);
       if (!again) break;
     }
     if (rcnt != 0u) issue_batch();
@@ -559,27 +559,25 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       if (stored_prev) wait_vm<1>();
       else wait_vm<0>();
       if (nstate == 1u) nstate = 2u;  // the next desk's loads are in
-      ckind = nkind;
+      ck = nk;
       cs = ns;
-      cused = nused;
       cb_pw = nb_pw;
       cb_inj = nb_inj;
       cb_id = nb_id;
       cb_j = nb_j;
-      csplit = nsplit;
       const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));  // (rides with the slot's reads)
       pp.read(W);
-      if (ckind == kWSeg && (cs.fl & kSAux)) ax = lds_ld4(SegAuxAddr(w));
+      if ((ck & 3u) == kWSeg && (cs.fl & kSAux)) ax = lds_ld4(SegAuxAddr(w));
       pp.release();
       idle = uni(idle_w);
     } else {
-      ckind = kWNone;
+      ck = kWNone;
     }
+    const uint32_t ckind = ck & 3u;
     // (no path into decide carries a desk load in flight: see loads_landed)
     loads_landed(na);
     loads_landed(nn);
     loads_landed(ni);
-    loads_landed(pfinit);
     LP_T(t1);
     decide();
     LP_T(t2);
@@ -633,6 +631,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       }
     } else if (ckind == kWBatch) {
       // ---- a batch of pieces, each on its own lanes ----
+      const uint32_t cused = (ck >> 2) & 127u, csplit = ck >> 9;
       const bool live = l < cused;
       const PW pw{cb_pw};
       const uint32_t j = cb_j, nl = pw.nl(), r = pw.r();
@@ -705,10 +704,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       // and take the next long span when this one is about to end (not
       // earlier: another wave may be idle)
       if (nstate == 2u && !nsorted) sort_desk();
-      if (!pfvalid && (!lvalid || lt + 1u >= PL_m(lpl))) {
-        if (dlong != 0u) take_own();
-        else pop();
-      }
       if (idle != 0u && (dlong | nlong) != 0u) share();
     }
     // the next desk's descriptor loads go out after this iteration's DMA and
@@ -723,10 +718,10 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     LP_ACC(4, ckind == kWSeg ? 1u : 0u);
     LP_ACC(5, ckind == kWBatch ? 1u : 0u);
     LP_ACC(6, ckind == kWNone ? 1u : 0u);
-    if (nkind == kWNone) {
+    if ((nk & 3u) == kWNone) {
       // (decide gives up after 64 steps -- e.g. desks of empty spans -- with
       // work left: decide again)
-      const bool left = nstate != 0u || !exhausted || dshort != 0u || rcnt != 0u || lvalid || pfvalid;
+      const bool left = nstate != 0u || !exhausted || dshort != 0u || rcnt != 0u || lvalid;
       if (!have && !left) break;
       have = false;
       continue;
