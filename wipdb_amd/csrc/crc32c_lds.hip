@@ -38,6 +38,14 @@
 
 #include "crc32c_dev.h"
 
+// The batch DMA: 1 = every lane loads its own stripe's 4 chunks (per-lane
+// addresses, no exchange); 0 = the segment DMA's layout (lane m of
+// instruction q loads chunk m % 4 of stripe 16 q + m / 4, addresses
+// exchanged by ds_bpermute) -- an A/B build.
+#ifndef WIPDB_LP_OWN_STRIPE_DMA
+#define WIPDB_LP_OWN_STRIPE_DMA 1
+#endif
+
 namespace wipdb {
 namespace lk {
 
@@ -165,8 +173,10 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     k1b |= (128u + 4u * t) << (8 * j);
     k2b |= (8u * t) << (8 * j);
   }
+#if !WIPDB_LP_OWN_STRIPE_DMA
   const uint32_t dsl = l >> 2;                          // stripe lane 16 q + dsl
   const uint32_t dci = ((l & 3u) - (l >> 4)) & 3u;      // chunk of that stripe
+#endif
 
   // ---- the piece ring: entry q in lane q ----
   uint32_t rp_lo = 0, rp_hi = 0, rpw = 0, rinj = 0, rid = 0;
@@ -456,6 +466,16 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint64_t S = sbase + ((static_cast<uint64_t>(b_hi) << 32) | b_lo) +
                        static_cast<uint64_t>(sp.s);
     const uint32_t s_lo = static_cast<uint32_t>(S), s_hi = static_cast<uint32_t>(S >> 32);
+#if WIPDB_LP_OWN_STRIPE_DMA
+    // instruction q: lane l DMAs chunk q of its own stripe into slot byte
+    // 1024 q + 16 l (no address exchange; the loop top reads the batch's
+    // stripes back lane-linear, conflict-free)
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint64_t a = S + static_cast<uint64_t>(StripeChunkSrc(sp.info, q));
+      if (live) dma1v(a, pp.slot + 1024u * q);
+    }
+#else
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
       const uint32_t sl = 16u * q + dsl;
@@ -464,6 +484,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
                          static_cast<uint64_t>(StripeChunkSrc(x_in, dci));
       if (sl < used) dma1v(a, pp.slot + 1024u * q);
     }
+#endif
     nb_pw = pw.v;
     nb_inj = b_inj;
     nb_id = b_id;
@@ -539,6 +560,61 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (rcnt != 0u) issue_batch();
   };
 
+  // One full 4 KiB segment of a long span (the iteration described by c,
+  // its 64 stripes in W): chained, pushed to the ring (a back piece follows)
+  // or finished (stored: returns true).
+  auto seg_compute = [&](const SegW& c, uint32_t (&W)[16], const u32x4& ax) -> bool {
+      // ---- one full 4 KiB segment of a long span ----
+      const uint32_t hp = c.hw & 15u, ws = (c.hw >> 4) & 3u;
+      if (c.fl & kSFirst) {
+        const uint32_t inj = head_register(l, c.init, hp);
+        if ((hp | ws) == 0u) {
+          W[0] ^= l == 0u ? inj : 0u;
+        } else {
+          uint32_t h4[4] = {W[0], W[1], W[2], W[3]};
+          fix_head(h4, hp, ws, inj);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) W[i] = l == 0u ? h4[i] : W[i];
+        }
+      } else {
+        W[0] ^= l == 0u ? chain : 0u;
+      }
+      if (kV && (c.fl & kSLast) && !(c.fl & kSPush)) {
+        uint32_t lo = W[14], hi = W[15];
+        fix_trailer(lo, hi, (c.hw >> 8) & 3u);
+        W[14] = l == 63u ? lo : W[14];
+        W[15] = l == 63u ? hi : W[15];
+      }
+      uint32_t R = fold<1>(lk, l, scan(lk, W))[0];
+      if (!(c.fl & kSLast)) {
+        chain = R;
+        return false;
+      }
+      if (c.fl & kSPush) {
+        // the back piece enters the ring with the segments' register
+        const bool me = l == rcnt;
+        rp_lo = me ? static_cast<uint32_t>(c.p0) : rp_lo;
+        rp_hi = me ? static_cast<uint32_t>(c.p0 >> 32) : rp_hi;
+        rpw = me ? c.pw : rpw;
+        rinj = me ? R : rinj;
+        rid = me ? c.id : rid;
+        ++rcnt;
+        rlanes += PW{c.pw}.nl();
+        return false;
+      }
+      {
+        if (c.fl & kSAux) {
+          const uint32_t tw = uni(ax.w);  // the aux chunk ends at E4 + 4
+          R = uni(tail_step(lk, R, tw, (c.hw >> 6) & 3u));
+        }
+        if (l == 0u) {
+          if (kV) out8[c.id] = R == verify_residue((c.hw >> 8) & 3u) ? 1u : 0u;
+          else out32[c.id] = msk ? mask_crc(~R) : ~R;
+        }
+      }
+      return true;
+  };
+
   // The loop: wait for this iteration's bytes, read them, issue the next
   // iteration's DMA (decide), compute this one.  An iteration that ends the
   // work may have pushed the last pieces: the loop then decides once more
@@ -551,6 +627,32 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   LP_T(t_start);
 #endif
   for (;;) {
+    // ---- the desk's single-segment spans back to back (aligned 4 KiB
+    // blocks, table blocks' main segments, verify blocks): a loop of its own,
+    // with only what they need live -- entered with such a segment issued,
+    // left with one issued (the general loop below takes it) ----
+    if (have && (nk & 3u) == kWSeg && (ns.fl & (kSFirst | kSLast | kSAux)) == (kSFirst | kSLast)) {
+      bool fidle = false;
+#pragma nounroll
+      for (;;) {
+        if (dlong == 0u || rcnt >= 62u || fidle) break;
+        if (rlanes + ((ns.fl & kSPush) ? PW{ns.pw}.nl() : 0u) >= 64u) break;  // a batch is due
+        const uint32_t pl = rdlane(dpl, static_cast<uint32_t>(__builtin_ctz(dlong)));
+        if (PL_m(pl) != 1u || PL_aux(pl) != 0u) break;
+        if (stored_prev) wait_vm<1>();
+        else wait_vm<0>();
+        if (nstate == 1u) nstate = 2u;
+        const SegW c = ns;
+        const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));
+        uint32_t W[16];
+        pp.read(W);
+        pp.release();
+        take_own();
+        issue_seg();
+        stored_prev = seg_compute(c, W, u32x4{0, 0, 0, 0});
+        fidle = uni(idle_w) != 0u;
+      }
+    }
     LP_T(t0);
     uint32_t W[16];
     uint32_t idle = 0;  // waves of the workgroup out of work
@@ -566,7 +668,22 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       cb_id = nb_id;
       cb_j = nb_j;
       const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));  // (rides with the slot's reads)
+#if WIPDB_LP_OWN_STRIPE_DMA
+      if ((ck & 3u) == kWBatch) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u32x4 d = lds_ld4(pp.slot + 16u * l + 1024u * q);
+          W[4 * q] = d.x;
+          W[4 * q + 1] = d.y;
+          W[4 * q + 2] = d.z;
+          W[4 * q + 3] = d.w;
+        }
+      } else {
+        pp.read(W);
+      }
+#else
       pp.read(W);
+#endif
       if ((ck & 3u) == kWSeg && (cs.fl & kSAux)) ax = lds_ld4(SegAuxAddr(w));
       pp.release();
       idle = uni(idle_w);
@@ -584,51 +701,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
 
     bool did_store = false;
     if (ckind == kWSeg) {
-      // ---- one full 4 KiB segment of a long span ----
-      const uint32_t hp = cs.hw & 15u, ws = (cs.hw >> 4) & 3u;
-      if (cs.fl & kSFirst) {
-        const uint32_t inj = head_register(l, cs.init, hp);
-        if ((hp | ws) == 0u) {
-          W[0] ^= l == 0u ? inj : 0u;
-        } else {
-          uint32_t c[4] = {W[0], W[1], W[2], W[3]};
-          fix_head(c, hp, ws, inj);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) W[i] = l == 0u ? c[i] : W[i];
-        }
-      } else {
-        W[0] ^= l == 0u ? chain : 0u;
-      }
-      if (kV && (cs.fl & kSLast) && !(cs.fl & kSPush)) {
-        uint32_t lo = W[14], hi = W[15];
-        fix_trailer(lo, hi, (cs.hw >> 8) & 3u);
-        W[14] = l == 63u ? lo : W[14];
-        W[15] = l == 63u ? hi : W[15];
-      }
-      uint32_t R = fold<1>(lk, l, scan(lk, W))[0];
-      if (!(cs.fl & kSLast)) {
-        chain = R;
-      } else if (cs.fl & kSPush) {
-        // the back piece enters the ring with the segments' register
-        const bool me = l == rcnt;
-        rp_lo = me ? static_cast<uint32_t>(cs.p0) : rp_lo;
-        rp_hi = me ? static_cast<uint32_t>(cs.p0 >> 32) : rp_hi;
-        rpw = me ? cs.pw : rpw;
-        rinj = me ? R : rinj;
-        rid = me ? cs.id : rid;
-        ++rcnt;
-        rlanes += PW{cs.pw}.nl();
-      } else {
-        if (cs.fl & kSAux) {
-          const uint32_t tw = uni(ax.w);  // the aux chunk ends at E4 + 4
-          R = uni(tail_step(lk, R, tw, (cs.hw >> 6) & 3u));
-        }
-        did_store = true;
-        if (l == 0u) {
-          if (kV) out8[cs.id] = R == verify_residue((cs.hw >> 8) & 3u) ? 1u : 0u;
-          else out32[cs.id] = msk ? mask_crc(~R) : ~R;
-        }
-      }
+      did_store = seg_compute(cs, W, ax);
     } else if (ckind == kWBatch) {
       // ---- a batch of pieces, each on its own lanes ----
       const uint32_t cused = (ck >> 2) & 127u, csplit = ck >> 9;
