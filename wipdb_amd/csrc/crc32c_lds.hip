@@ -42,8 +42,10 @@
 // addresses, no exchange); 0 = the segment DMA's layout (lane m of
 // instruction q loads chunk m % 4 of stripe 16 q + m / 4, addresses
 // exchanged by ds_bpermute) -- an A/B build.
+// (own stripes measured slower on every short bucket: the uncoalesced DMA
+// instructions cost more than the exchange, profiles/r03g_ab.log)
 #ifndef WIPDB_LP_OWN_STRIPE_DMA
-#define WIPDB_LP_OWN_STRIPE_DMA 1
+#define WIPDB_LP_OWN_STRIPE_DMA 0
 #endif
 
 namespace wipdb {
@@ -112,6 +114,14 @@ __device__ __forceinline__ uint32_t head_register_lane(uint32_t l, uint32_t init
     }
   }
   return init == 0u ? h0 : r;
+}
+
+// verify_residue(jv) for a run-time jv (the constants, selected: the
+// constexpr function itself would run its bit loop per span)
+__device__ __forceinline__ uint32_t residue_of(uint32_t jv) {
+  constexpr uint32_t kRes0 = verify_residue(0), kRes1 = verify_residue(1),
+                     kRes2 = verify_residue(2), kRes3 = verify_residue(3);
+  return jv == 0u ? kRes0 : (jv == 1u ? kRes1 : (jv == 2u ? kRes2 : kRes3));
 }
 
 // Word e / 4 .. of the 16 bytes c0..c3 at byte e (per lane; e + 4 may pass
@@ -608,7 +618,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
           R = uni(tail_step(lk, R, tw, (c.hw >> 6) & 3u));
         }
         if (l == 0u) {
-          if (kV) out8[c.id] = R == verify_residue((c.hw >> 8) & 3u) ? 1u : 0u;
+          if (kV) out8[c.id] = R == residue_of((c.hw >> 8) & 3u) ? 1u : 0u;
           else out32[c.id] = msk ? mask_crc(~R) : ~R;
         }
       }
@@ -627,18 +637,19 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   LP_T(t_start);
 #endif
   for (;;) {
-    // ---- the desk's single-segment spans back to back (aligned 4 KiB
-    // blocks, table blocks' main segments, verify blocks): a loop of its own,
-    // with only what they need live -- entered with such a segment issued,
-    // left with one issued (the general loop below takes it) ----
-    if (have && (nk & 3u) == kWSeg && (ns.fl & (kSFirst | kSLast | kSAux)) == (kSFirst | kSLast)) {
+    // ---- segments back to back: the long span in hand, then the desk's
+    // own spans with segments (aligned 4 KiB blocks, table blocks' main
+    // segments, verify blocks, long spans) -- a loop of its own, with only
+    // what they need live.  Entered with a segment issued, left with one
+    // issued (the general loop below takes it): when a batch is due, the
+    // desk has no span with segments left, or another wave is idle while
+    // this one holds long spans (the general loop shares them). ----
+    if (have && (nk & 3u) == kWSeg) {
       bool fidle = false;
 #pragma nounroll
       for (;;) {
-        if (dlong == 0u || rcnt >= 62u || fidle) break;
-        if (rlanes + ((ns.fl & kSPush) ? PW{ns.pw}.nl() : 0u) >= 64u) break;  // a batch is due
-        const uint32_t pl = rdlane(dpl, static_cast<uint32_t>(__builtin_ctz(dlong)));
-        if (PL_m(pl) != 1u || PL_aux(pl) != 0u) break;
+        if (!lvalid && (dlong == 0u || fidle)) break;
+        if (rcnt >= 62u || rlanes + ((ns.fl & kSPush) ? PW{ns.pw}.nl() : 0u) >= 64u) break;  // a batch is due
         if (stored_prev) wait_vm<1>();
         else wait_vm<0>();
         if (nstate == 1u) nstate = 2u;
@@ -646,10 +657,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));
         uint32_t W[16];
         pp.read(W);
+        u32x4 fax{0, 0, 0, 0};
+        if (c.fl & kSAux) fax = lds_ld4(SegAuxAddr(w));
         pp.release();
-        take_own();
+        if (!lvalid) take_own();
         issue_seg();
-        stored_prev = seg_compute(c, W, u32x4{0, 0, 0, 0});
+        stored_prev = seg_compute(c, W, fax);
         fidle = uni(idle_w) != 0u;
       }
     }
@@ -758,11 +771,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       carry_tw = t_new;
       const bool fin = leader && done;
       if (kV) {
-        constexpr uint32_t kRes0 = verify_residue(0), kRes1 = verify_residue(1),
-                           kRes2 = verify_residue(2), kRes3 = verify_residue(3);
-        const uint32_t jv = pw.jv();
-        const uint32_t res = jv == 0u ? kRes0 : (jv == 1u ? kRes1 : (jv == 2u ? kRes2 : kRes3));
-        if (fin) out8[cb_id] = G == res ? 1u : 0u;
+        if (fin) out8[cb_id] = G == residue_of(pw.jv()) ? 1u : 0u;
       } else {
         const uint32_t Gt = tail_step(lk, G, twv, pw.k());
         G = pw.x() ? Gt : G;
