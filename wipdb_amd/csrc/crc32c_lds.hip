@@ -14,7 +14,7 @@
 //     global_load_lds_dwordx4, nontemporal) while it computes the current
 //     one, and lane l CRCs the 64-byte stripe [64 l, 64 l + 64) of it
 //     (slicing-by-4 on the rotated LDS tables, crc32c_dev.h);
-//   * spans come in DESKS of 16 (one LDS atomic on the workgroup's unit
+//   * spans come in DESKS of 32 (one LDS atomic on the workgroup's unit
 //     counter, the descriptors vector-loaded a desk ahead, one span per
 //     lane), planned per lane (crc32c_plan.h): m full 4 KiB segments from
 //     the start of the span's grid, then a back piece of the remaining
@@ -50,6 +50,10 @@
 
 namespace wipdb {
 namespace lk {
+
+// ---------------------------------------------------------------------------
+// Spans per desk (lanes 0 .. kDesk - 1 hold a desk; masks are 32 bits)
+constexpr uint32_t kDesk = 32;
 
 // ---------------------------------------------------------------------------
 // Wave scans (row-local DPP steps, rows joined through readlane)
@@ -164,7 +168,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   const uint32_t l = lane_tid() & 63u;
   const uint32_t w = uni(lane_tid() >> 6);
   const uint64_t count = src.count;
-  if (static_cast<uint64_t>(group_id()) * 16u >= count) return;  // no desk of work
+  if (static_cast<uint64_t>(group_id()) * kDesk >= count) return;  // no desk of work
   load_image(image, w, l);
   const Lane lk = make_lane<1>(l);
   Pipe pp;
@@ -191,7 +195,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // ---- the piece ring: entry q in lane q ----
   uint32_t rp_lo = 0, rp_hi = 0, rpw = 0, rinj = 0, rid = 0;
   uint32_t rcnt = 0, rlanes = 0;
-  // ---- the desk (lanes 0..15) and the next desk, loading ----
+  // ---- the desk (lanes 0 .. kDesk - 1) and the next desk, loading ----
   uint64_t da = 0, na = 0;
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
   uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words (switch_desk)
@@ -220,13 +224,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t carry = 0, carry_tw = 0;   // the split piece's register over its first lanes, tail word
   uint32_t chain = 0;
 
-  // A desk of 16 spans: one unit-counter add, the descriptors loaded (lanes
-  // 0..15; waited for at first use).
+  // A desk of kDesk spans: one unit-counter add, the descriptors loaded
+  // (lanes 0 .. kDesk - 1; waited for at first use).
   auto grab_desk = [&]() {
     uint32_t u = 0;
-    if (l == 0u) u = lds_add(MiscAddr(kMiscUnit), 16u);
+    if (l == 0u) u = lds_add(MiscAddr(kMiscUnit), kDesk);
     u = uni(u);
-    const uint64_t nb64 = (static_cast<uint64_t>(u >> 4) * group_count() + group_id()) * 16u;
+    const uint64_t nb64 = (static_cast<uint64_t>(u / kDesk) * group_count() + group_id()) * kDesk;
     nbase = static_cast<uint32_t>(nb64);
     if (nb64 >= count) {
       exhausted = true;
@@ -234,7 +238,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       return;
     }
     const uint64_t s = nb64 + l;
-    const bool v = l < 16u && s < count;
+    const bool v = l < kDesk && s < count;
     nlive = static_cast<uint32_t>(ballot(v));
     if (v) src.lane(s, na, nn, ni);
     if (l == 0u) lds_add(MiscAddr(kMiscDesks), 1u);
@@ -293,7 +297,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // The long spans of desk lanes m (a, bytes b, span base + lane) into the
   // queue; they leave the workgroup's held count once queued.
   auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint32_t base, uint32_t held) {
-    const bool lng = l < 16u && ((m >> (l & 15u)) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
+    const bool lng = l < kDesk && ((m >> (l & (kDesk - 1u))) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
     const uint32_t k = static_cast<uint32_t>(__builtin_popcount(m));
     uint32_t q = 0;
     if (l == 0u) q = lds_add(MiscAddr(kMiscQTail), k);
@@ -322,7 +326,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // this wave, counted in the workgroup's held count before the desk leaves
   // the in-flight count).
   auto sort_desk = [&]() {
-    const bool live = l < 16u && ((nlive >> (l & 15u)) & 1u) != 0u;
+    const bool live = l < kDesk && ((nlive >> (l & (kDesk - 1u))) & 1u) != 0u;
     const uint64_t s = static_cast<uint64_t>(nbase) + l;
     const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
     const bool empty = live && p.empty;
@@ -395,14 +399,14 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint64_t p0 = da - hp;
     const uint32_t inj = head_register_lane(l, di, hp);
     const uint32_t rank = mbcnt_lo(dshort, 0u);
-    const bool tk = l < 16u && ((dshort >> (l & 15u)) & 1u) != 0u && rank < take;
+    const bool tk = l < kDesk && ((dshort >> (l & (kDesk - 1u))) & 1u) != 0u && rank < take;
     const uint32_t tmask = static_cast<uint32_t>(ballot(tk));
     const uint32_t nl_sum = scan_add(tk ? PW{dpw}.nl() : 0u, l);
     // ring lane q in [rcnt, rcnt + take) pulls the (q - rcnt)-th short lane
     const uint32_t kq = l - rcnt;
     uint32_t pos = 0;
 #pragma unroll
-    for (uint32_t st = 8; st != 0u; st >>= 1) {
+    for (uint32_t st = kDesk / 2u; st != 0u; st >>= 1) {  // (pos + st <= 31)
       const uint32_t below = dshort & ((1u << (pos + st)) - 1u);
       pos = static_cast<uint32_t>(__builtin_popcount(below)) <= kq ? pos + st : pos;
     }
