@@ -230,6 +230,11 @@ int main(int argc, char** argv) {
     auto in2 = inits_of(l2.size());
     RunSpans("shared long: 40 (inits)", buf, Packed(l2, 1, 5), l2, &in2, true, 2);
   }
+  if (Want(argc, argv, "queue full")) {  // one workgroup, more long spans than queue slots
+    auto l = lens_of(700, 16384, 24000);
+    auto in = inits_of(l.size());
+    RunSpans("queue full: 700 long (inits)", buf, Packed(l, 7, 5), l, &in, false, 1);
+  }
   if (Want(argc, argv, "zipf mix")) {
     const uint32_t B[] = {512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
     std::vector<uint32_t> l;

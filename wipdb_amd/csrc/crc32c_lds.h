@@ -71,13 +71,16 @@ constexpr uint32_t kMiscQTail = 274;
 constexpr uint32_t kMiscDesks = 275;   // desks grabbed, not sorted yet (run_lp)
 constexpr uint32_t kMiscIdle = 276;    // waves out of work, waiting for shared long spans
 constexpr uint32_t kMiscHeld = 277;    // long spans held by a wave, not taken or shared yet
+constexpr uint32_t kMiscQRes = 278;    // queue records pushed and not yet freed (<= kQSlots)
+constexpr uint32_t kMiscQInit = 576;   // 256 words: the init_crc of queue record k
 constexpr uint32_t kMiscBytes = 1024 * 4;
 
 // run_lp (the lane-packed spans / strided / verify kernels):
 //   * the workgroup's long-span queue: 256 records of 16 bytes in the a = 0
 //     column of the main rows (bytes 128..143 of row k; the list kernels
 //     keep their aux pieces there instead): {a_lo, a_hi, n, span + 1}, a
-//     last word of 0 = a free slot;
+//     last word of 0 = a free slot; record k's init_crc in misc word
+//     kMiscQInit + k;
 //   * wave w's aux chunk of a segment tail: the c = 0 column of level-2 row
 //     128 + w (misc words 512.. are unused).
 constexpr uint32_t kQSlots = 256;

@@ -54,6 +54,12 @@ namespace lk {
 // ---------------------------------------------------------------------------
 // Spans per desk (lanes 0 .. kDesk - 1 hold a desk; masks are 32 bits)
 constexpr uint32_t kDesk = 32;
+// Spans of this many segments or more are queued for the workgroup as soon
+// as their desk is sorted
+#ifndef WIPDB_LP_EAGER_SEGS
+#define WIPDB_LP_EAGER_SEGS 4
+#endif
+constexpr uint32_t kEagerSegs = WIPDB_LP_EAGER_SEGS;
 
 // ---------------------------------------------------------------------------
 // Wave scans (row-local DPP steps, rows joined through readlane)
@@ -278,15 +284,17 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     }
     compiler_barrier();  // the record after its marker
     const uint32_t r0 = uni(lds_ld_sync(ra)), r1 = uni(lds_ld_sync(ra + 4u)),
-                   r2 = uni(lds_ld_sync(ra + 8u));
+                   r2 = uni(lds_ld_sync(ra + 8u)),
+                   ri = uni(lds_ld_sync(MiscAddr(kMiscQInit + (idx & (kQSlots - 1u)))));
     lgkm_wait();  // read before the slot is freed
-    if (l == 0u) lds_st_sync(ra + 12u, 0u);
+    if (l == 0u) {
+      lds_st_sync(ra + 12u, 0u);
+      lds_add(MiscAddr(kMiscQRes), 0xffffffffu);
+    }
     if (r3 == 0u) return;  // never written (cannot happen; no hang if it does)
     const uint64_t a = (static_cast<uint64_t>(r1) << 32) | r0;
     lid = r3 - 1u;
-    // (0 without an init column; the strided blocks' init.  A stall on the
-    // load: shared spans are rare)
-    linit = uni(src.init_of(lid));
+    linit = ri;
     const Plan p = MakePlan(a, static_cast<uint32_t>(sbase + a), r2, kV);
     lpl = PackPL(p);
     lpw = p.pw;
@@ -294,15 +302,26 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     lt = 0;
     lvalid = true;
   };
-  // The long spans of desk lanes m (a, bytes b, span base + lane) into the
-  // queue; they leave the workgroup's held count once queued.
-  auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint32_t base, uint32_t held) {
+  // The long spans of desk lanes m (a, bytes b, init iv, span base + lane)
+  // into the queue, if it has room for them all (reserved in the QRes
+  // count, so a push never waits on a slot no wave will free); `held` of the
+  // workgroup's held count leave it once queued.  Returns whether queued.
+  auto queue_longs = [&](uint32_t m, uint64_t a, uint32_t b, uint32_t iv, uint32_t base,
+                         uint32_t held) -> bool {
     const bool lng = l < kDesk && ((m >> (l & (kDesk - 1u))) & 1u) != 0u;  // (a shift by >= 32 is mod 32)
     const uint32_t k = static_cast<uint32_t>(__builtin_popcount(m));
+    uint32_t rs = 0;
+    if (l == 0u) rs = lds_add(MiscAddr(kMiscQRes), k);
+    rs = uni(rs);
+    if (rs + k > kQSlots) {
+      if (l == 0u) lds_add(MiscAddr(kMiscQRes), 0u - k);
+      return false;
+    }
     uint32_t q = 0;
     if (l == 0u) q = lds_add(MiscAddr(kMiscQTail), k);
     q = uni(q);
-    const uint32_t ra = QRecAddr(q + mbcnt_lo(m, 0u));
+    const uint32_t qk = q + mbcnt_lo(m, 0u);
+    const uint32_t ra = QRecAddr(qk);
     // a slot is reused only once its last record has been read (queue
     // records are popped by the waves that asked for work: this rarely waits)
 #pragma nounroll
@@ -315,10 +334,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       lds_st_sync(ra, static_cast<uint32_t>(a));
       lds_st_sync(ra + 4u, static_cast<uint32_t>(a >> 32));
       lds_st_sync(ra + 8u, b);
+      lds_st_sync(MiscAddr(kMiscQInit + (qk & (kQSlots - 1u))), iv);
     }
     lgkm_wait();  // the record before its marker
     if (lng) lds_st_sync(ra + 12u, base + l + 1u);
-    if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0u - held);  // (after the records: in order)
+    if (l == 0u && held != 0u) lds_add(MiscAddr(kMiscHeld), 0u - held);  // (after the records: in order)
+    return true;
   };
 
   // The next desk, once its descriptors are in: its empty spans answered,
@@ -333,6 +354,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
     nshort = static_cast<uint32_t>(ballot(live && !p.empty && p.m == 0u));
     nlong = static_cast<uint32_t>(ballot(live && !p.empty && p.m != 0u));
+    // spans of kEagerSegs segments or more go to the queue right away (if it
+    // has room): the workgroup's waves take them one at a time, as they
+    // become free -- a desk of long spans is not left on one wave
+    const uint32_t big = static_cast<uint32_t>(ballot(live && !p.empty && p.m >= kEagerSegs));
+    if (big != 0u && queue_longs(big, na, src.bytes(nn), ni, nbase, 0u)) nlong &= ~big;
     if (l == 0u) {
       if (nlong != 0u) lds_add(MiscAddr(kMiscHeld), static_cast<uint32_t>(__builtin_popcount(nlong)));
       lds_add(MiscAddr(kMiscDesks), 0xffffffffu);
@@ -344,12 +370,13 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // (the desk's long spans leave the held count all at once: those it has
   // taken and those it queues now)
   auto share = [&]() {
-    if (dlong != 0u) queue_longs(dlong, da, dn, dbase, dtotal);
-    if (nstate == 2u && nsorted && nlong != 0u)
-      queue_longs(nlong, na, src.bytes(nn), nbase, static_cast<uint32_t>(__builtin_popcount(nlong)));
-    dlong = 0;
-    dtotal = 0;
-    nlong = 0;
+    if (dlong != 0u && queue_longs(dlong, da, dn, di, dbase, dtotal)) {
+      dlong = 0;
+      dtotal = 0;
+    }
+    if (nstate == 2u && nsorted && nlong != 0u &&
+        queue_longs(nlong, na, src.bytes(nn), ni, nbase, static_cast<uint32_t>(__builtin_popcount(nlong))))
+      nlong = 0;
   };
   // The desk's next own long span becomes the one being run; the desk's
   // long spans leave the held count when the last is taken.
