@@ -34,6 +34,9 @@ for s in $STEPS; do
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${P}_pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${P}_pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    bucket_pmc) run bucket_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${P}_bfetch -o run --output-format csv -- python3 scripts/bucket_traffic.py run &&
+                run bucket_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${P}_bwrite -o run --output-format csv -- python3 scripts/bucket_traffic.py run &&
+                python3 scripts/bucket_traffic.py summarize gpurun_out/${P}_bfetch gpurun_out/${P}_bwrite > gpurun_out/${P}_bucket_traffic.json; tail -40 gpurun_out/${P}_bucket_traffic.json ;;
     pmc_sq) run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM -d gpurun_out/${P}_pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s" ;;
   esac
