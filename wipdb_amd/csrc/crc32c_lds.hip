@@ -174,7 +174,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   const uint32_t l = lane_tid() & 63u;
   const uint32_t w = uni(lane_tid() >> 6);
   const uint64_t count = src.count;
-  if (static_cast<uint64_t>(group_id()) * kDesk >= count) return;  // no desk of work
+  if (static_cast<uint64_t>(group_id()) * 16u >= count) return;  // no block of work
   load_image(image, w, l);
   const Lane lk = make_lane<1>(l);
   Pipe pp;
@@ -205,7 +205,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint64_t da = 0, na = 0;
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
   uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words (switch_desk)
-  uint32_t dbase = 0, nbase = 0;  // (a launch holds < 2^31 spans)
+  uint32_t dbase = 0, nbase = 0;  // first unit of the desk (span_of: its span)
   uint32_t dtotal = 0;        // the desk's long spans still counted in the held count
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
   uint32_t dlong = 0;         // desk lanes whose long span this wave has not taken
@@ -230,23 +230,42 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t carry = 0, carry_tw = 0;   // the split piece's register over its first lanes, tail word
   uint32_t chain = 0;
 
-  // A desk of kDesk spans: one unit-counter add, the descriptors loaded
-  // (lanes 0 .. kDesk - 1; waited for at first use).
+  // The workgroup's units: unit u is span ((u / 16) * grid + wg) * 16 +
+  // u % 16 -- blocks of 16 spans round robin over the grid, so the chip
+  // reads one compact window of the batch at a time; ug = its unit count.
+  auto span_of = [&](uint32_t un) -> uint64_t {
+    return (static_cast<uint64_t>(un >> 4) * group_count() + group_id()) * 16u + (un & 15u);
+  };
+  uint32_t ug = 0;
+  {
+    const uint64_t nblk = (count + 15u) >> 4, g = group_id(), G = group_count();
+    const uint64_t nbg = (nblk - 1u - g) / G + 1u;  // (g < nblk: checked above)
+    const bool partial_last = (nblk - 1u) % G == g;
+    ug = static_cast<uint32_t>(nbg * 16u - (partial_last ? nblk * 16u - count : 0u));
+  }
+  // A desk: one unit-counter add, the descriptors loaded (lanes 0 .. size -
+  // 1; waited for at first use).  kDesk units while the workgroup has
+  // plenty left, then 16 and 8 (the waves' last desks end close together).
   auto grab_desk = [&]() {
-    uint32_t u = 0;
-    if (l == 0u) u = lds_add(MiscAddr(kMiscUnit), kDesk);
+    uint32_t u = 0, size = kDesk;
+    if (l == 0u) {
+      const uint32_t seen = lds_ld_sync(MiscAddr(kMiscUnit));
+      const uint32_t rem = seen < ug ? ug - seen : 0u;
+      size = rem >= 32u * kDesk ? kDesk : (rem >= 16u * kDesk ? kDesk / 2u : kDesk / 4u);
+      u = lds_add(MiscAddr(kMiscUnit), size);
+    }
     u = uni(u);
-    const uint64_t nb64 = (static_cast<uint64_t>(u / kDesk) * group_count() + group_id()) * kDesk;
-    nbase = static_cast<uint32_t>(nb64);
-    if (nb64 >= count) {
+    size = uni(size);
+    nbase = u;
+    if (u >= ug) {
       exhausted = true;
       nstate = 0;
       return;
     }
-    const uint64_t s = nb64 + l;
-    const bool v = l < kDesk && s < count;
+    const uint32_t un = u + l;
+    const bool v = l < size && un < ug;
     nlive = static_cast<uint32_t>(ballot(v));
-    if (v) src.lane(s, na, nn, ni);
+    if (v) src.lane(span_of(un), na, nn, ni);
     if (l == 0u) lds_add(MiscAddr(kMiscDesks), 1u);
     nstate = 1;
     nsorted = false;
@@ -337,7 +356,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       lds_st_sync(MiscAddr(kMiscQInit + (qk & (kQSlots - 1u))), iv);
     }
     lgkm_wait();  // the record before its marker
-    if (lng) lds_st_sync(ra + 12u, base + l + 1u);
+    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(span_of(base + l)) + 1u);
     if (l == 0u && held != 0u) lds_add(MiscAddr(kMiscHeld), 0u - held);  // (after the records: in order)
     return true;
   };
@@ -348,7 +367,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // the in-flight count).
   auto sort_desk = [&]() {
     const bool live = l < kDesk && ((nlive >> (l & (kDesk - 1u))) & 1u) != 0u;
-    const uint64_t s = static_cast<uint64_t>(nbase) + l;
+    const uint64_t s = span_of(nbase + l);
     const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
     const bool empty = live && p.empty;
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
@@ -388,7 +407,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     lpl = pl;
     lpw = rdlane(dpw, k);
     linit = rdlane(di, k);
-    lid = dbase + k;
+    lid = static_cast<uint32_t>(span_of(dbase + k));
     lt = 0;
     lvalid = true;
     dlong &= dlong - 1u;
@@ -441,7 +460,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t v_lo = bperm(static_cast<uint32_t>(p0), pos);
     const uint32_t v_hi = bperm(static_cast<uint32_t>(p0 >> 32), pos);
     const uint32_t v_pw = bperm(dpw, pos), v_inj = bperm(inj, pos);
-    const uint32_t v_id = dbase + pos;
+    const uint32_t v_id = static_cast<uint32_t>(span_of(dbase + pos));
     rp_lo = me ? v_lo : rp_lo;
     rp_hi = me ? v_hi : rp_hi;
     rpw = me ? v_pw : rpw;

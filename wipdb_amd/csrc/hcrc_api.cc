@@ -334,9 +334,9 @@ class LaneLease {
 constexpr size_t kMaxLaunchSpans = size_t(1) << 31;
 
 // LDS-staged kernels: one workgroup per CU, but no more than the batch's
-// 32-span desks (a workgroup's desks are w, w + grid, ...).
+// 16-span blocks (a workgroup's units are blocks w, w + grid, ...).
 int LdsGrid(hcrc_ctx* ctx, size_t count) {
-  const size_t need = (count + 31) / 32;
+  const size_t need = (count + 15) / 16;
   return static_cast<int>(std::max<size_t>(std::min<size_t>(need, size_t(ctx->num_cu)), 1));
 }
 
