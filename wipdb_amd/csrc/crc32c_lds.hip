@@ -626,18 +626,20 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   auto seg_compute = [&](const SegW& c, uint32_t (&W)[16], const u32x4& ax) -> bool {
       // ---- one full 4 KiB segment of a long span ----
       const uint32_t hp = c.hw & 15u, ws = (c.hw >> 4) & 3u;
-      if (c.fl & kSFirst) {
-        const uint32_t inj = head_register(l, c.init, hp);
-        if ((hp | ws) == 0u) {
-          W[0] ^= l == 0u ? inj : 0u;
+      {
+        // lane 0's first chunk: the head (masked, shifted, the head register
+        // injected) or the chain register -- computed aside, selected in
+        // (one register assignment of W whichever branch ran)
+        uint32_t h4[4] = {W[0], W[1], W[2], W[3]};
+        if (c.fl & kSFirst) {
+          const uint32_t inj = head_register(l, c.init, hp);
+          if ((hp | ws) == 0u) h4[0] ^= inj;
+          else fix_head(h4, hp, ws, inj);
         } else {
-          uint32_t h4[4] = {W[0], W[1], W[2], W[3]};
-          fix_head(h4, hp, ws, inj);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) W[i] = l == 0u ? h4[i] : W[i];
+          h4[0] ^= chain;
         }
-      } else {
-        W[0] ^= l == 0u ? chain : 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) W[i] = l == 0u ? h4[i] : W[i];
       }
       if (kV && (c.fl & kSLast) && !(c.fl & kSPush)) {
         uint32_t lo = W[14], hi = W[15];
