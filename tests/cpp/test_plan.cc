@@ -53,7 +53,7 @@ uint32_t HeadRegister(uint32_t init, uint32_t h) {
 }
 uint32_t Mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
 
-int g_fail = 0, g_cases = 0, g_pieces = 0, g_segs = 0, g_partial = 0;
+int g_fail = 0, g_cases = 0, g_pieces = 0, g_segs = 0;
 uint32_t g_max_nl = 0;
 
 struct Case {
@@ -91,32 +91,20 @@ struct Case {
     const uint32_t residue = verify ? verify_residue(p.jv) : 0u;
     // ---- full segments, from the start ----
     uint32_t R = 0;
-    if (p.front) {
-      ++g_partial;
-      if (p.pw != 0u || p.front >= 256u - kPartialMin + 1u || 256u - p.front != (p.C & 255u)) {
-        fprintf(stderr, "  bad partial plan (front %u, C %u, pw %#x)\n", p.front, p.C, p.pw);
-        ++g_fail;
-      }
-    }
     for (uint32_t t = 0; t < p.m; ++t) {
       ++g_segs;
       uint8_t win[4096];
-      // (a partial first window starts `front` chunks in front of chunk 0)
-      const uint64_t wb = sbase + p.c0 - 16u * uint64_t(p.front) + 4096u * uint64_t(t);
-      const uint32_t f = t == 0u ? p.front : 0u;
+      const uint64_t wb = sbase + p.c0 + 4096u * uint64_t(t);
       for (uint32_t c = 0; c < 256; ++c) {
-        // the segment DMA: chunk 0 of segment 0 is read ws words late, the
-        // window chunks in front of it re-read it
-        const uint32_t lim = 16u * f + 4u * p.ws;
-        const uint32_t o = t == 0u ? (16u * c > lim ? 16u * c : lim) : 16u * c;
+        // the segment DMA: lane 0's chunk 0 of segment 0 is read ws words late
+        const uint32_t o = (t == 0u && c == 0u) ? 4u * p.ws : 16u * c;
         memcpy(win + 16 * c, Read(wb + o, 16), 16);
       }
       if (t == 0u) {
         uint32_t c4[4];
-        memcpy(c4, win + 16 * f, 16);
+        memcpy(c4, win, 16);
         fix_head(c4, p.hp, p.ws, HeadRegister(init, p.hp));
-        memset(win, 0, 16u * f);
-        memcpy(win + 16 * f, c4, 16);
+        memcpy(win, c4, 16);
       } else {
         uint32_t w0;
         memcpy(&w0, win, 4);
@@ -289,9 +277,7 @@ int main() {
       const uint64_t sbase = (seed >> 33) & 1 ? (s & ~uint64_t(4095)) : B;
       Check(buf, sbase, s, n, init);
     }
-  // (the largest piece: kPartialMin - 1 chunks + the aux chunk)
-  const uint32_t want_nl = (kPartialMin + 3u) / 4u;
-  printf("%s: %d cases, %d pieces (max %u lanes, want %u), %d segments (%d partial first), %d failures\n",
-         g_fail ? "FAIL" : "PASS", g_cases, g_pieces, g_max_nl, want_nl, g_segs, g_partial, g_fail);
-  return g_fail || g_max_nl > want_nl || g_max_nl + 4u < want_nl || g_partial == 0 ? 1 : 0;
+  printf("%s: %d cases, %d pieces (max %u lanes), %d segments, %d failures\n",
+         g_fail ? "FAIL" : "PASS", g_cases, g_pieces, g_max_nl, g_segs, g_fail);
+  return g_fail || g_max_nl != 64u ? 1 : 0;
 }

@@ -316,8 +316,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     linit = ri;
     const Plan p = MakePlan(a, static_cast<uint32_t>(sbase + a), r2, kV);
     lpl = PackPL(p);
-    lpw = PlanPW(p);
-    lc0 = p.c0 - 16u * p.front;  // the first window's origin
+    lpw = p.pw;
+    lc0 = p.c0;
     lt = 0;
     lvalid = true;
   };
@@ -406,7 +406,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
            rdlane(static_cast<uint32_t>(da), k)) - PL_hp(pl);
     lpl = pl;
     lpw = rdlane(dpw, k);
-    lc0 -= 16u * PW_front(lpw);  // the first window's origin
     linit = rdlane(di, k);
     lid = static_cast<uint32_t>(span_of(dbase + k));
     lt = 0;
@@ -423,7 +422,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     {
       const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
       dpl = PackPL(p);
-      dpw = PlanPW(p);
+      dpw = p.pw;
     }
     da = na;
     dn = src.bytes(nn);
@@ -478,25 +477,16 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint64_t p0 = lc0 + 4096u * static_cast<uint64_t>(m);  // the back piece / span grid end
     const uint64_t wb = sbase + lc0 + 4096u * static_cast<uint64_t>(lt);
     const uint32_t o = 16u * pp.cm;
-    const uint32_t front = lt == 0u ? PW_front(lpw) : 0u;
-    if (front == 0u) {
-      const uint32_t s0 = lt == 0u ? 4u * PL_ws(lpl) : 0u;
-      dma4(wb, pp.slot, o > s0 ? o : s0, o + 1024u, o + 2048u, o + 3072u);
-    } else {
-      // a partial first window: its chunks in front of chunk 0 re-read
-      // chunk 0 (zeroed later), chunk 0 read ws words late
-      const uint32_t s0 = 16u * front + 4u * PL_ws(lpl);
-      dma4(wb, pp.slot, o > s0 ? o : s0, o + 1024u > s0 ? o + 1024u : s0,
-           o + 2048u > s0 ? o + 2048u : s0, o + 3072u > s0 ? o + 3072u : s0);
-    }
+    const uint32_t s0 = lt == 0u ? 4u * PL_ws(lpl) : 0u;
+    dma4(wb, pp.slot, o > s0 ? o : s0, o + 1024u, o + 2048u, o + 3072u);
     const bool last = lt + 1u == m;
     const bool aux = last && PL_aux(lpl) != 0u;
     ns.fl = (lt == 0u ? kSFirst : 0u) | (last ? kSLast : 0u) |
-            (last && PW_piece(lpw) ? kSPush : 0u) | (aux ? kSAux : 0u);
+            (last && lpw != 0u ? kSPush : 0u) | (aux ? kSAux : 0u);
     // (seg_aux: no piece, so the grid ends at c0 + 4096 m; the aux chunk is
     // the 16 bytes ending at E4 + 4)
     if (aux) dma_piece(l, sbase + p0 - 12u, 0u, SegAuxAddr(w));
-    ns.hw = PL_hw(lpl) | (front << 10);
+    ns.hw = PL_hw(lpl);
     ns.init = linit;
     ns.id = lid;
     ns.pw = lpw;
@@ -640,37 +630,16 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         // lane 0's first chunk: the head (masked, shifted, the head register
         // injected) or the chain register -- computed aside, selected in
         // (one register assignment of W whichever branch ran)
-        const uint32_t front = (c.hw >> 10) & 255u;
-        if (front == 0u) {
-          uint32_t h4[4] = {W[0], W[1], W[2], W[3]};
-          if (c.fl & kSFirst) {
-            const uint32_t inj = head_register(l, c.init, hp);
-            if ((hp | ws) == 0u) h4[0] ^= inj;
-            else fix_head(h4, hp, ws, inj);
-          } else {
-            h4[0] ^= chain;
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) W[i] = l == 0u ? h4[i] : W[i];
-        } else {
-          // a partial first window: chunk 0 is window chunk `front` (lane
-          // front / 4, its chunk front % 4); the chunks in front are zeroed
+        uint32_t h4[4] = {W[0], W[1], W[2], W[3]};
+        if (c.fl & kSFirst) {
           const uint32_t inj = head_register(l, c.init, hp);
-          const uint32_t lf = front >> 2, cf = front & 3u;
-          uint32_t h4[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            h4[q] = cf == 0u ? W[q] : (cf == 1u ? W[4 + q] : (cf == 2u ? W[8 + q] : W[12 + q]));
-          fix_head(h4, hp, ws, inj);
-#pragma unroll
-          for (uint32_t i = 0; i < 4; ++i)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const bool z = l < lf || (l == lf && i < cf);
-              const bool h = l == lf && i == cf;
-              W[4 * i + q] = z ? 0u : (h ? h4[q] : W[4 * i + q]);
-            }
+          if ((hp | ws) == 0u) h4[0] ^= inj;
+          else fix_head(h4, hp, ws, inj);
+        } else {
+          h4[0] ^= chain;
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) W[i] = l == 0u ? h4[i] : W[i];
       }
       if (kV && (c.fl & kSLast) && !(c.fl & kSPush)) {
         uint32_t lo = W[14], hi = W[15];

@@ -23,13 +23,8 @@
 // The plan.  m = C / 256 full segments FROM THE START of the grid (segment t
 // = chunks [256 t, 256 t + 256), one wave iteration each, chained by the
 // register; segment 0 carries the head), then a BACK PIECE of r = C mod 256
-// chunks (a span of fewer than 256 chunks is all piece, head included) --
-// or, when r >= kPartialMin (a piece that would fill most of a batch, which
-// costs ~1.7 segment iterations), a PARTIAL FIRST SEGMENT instead: the
-// window of 256 chunks ending at chunk r, its front = 256 - r chunks zeroed
-// and the head injected at chunk 0 inside it, then the m full segments
-// (m + 1 in all, no piece).
-// A piece does not get a 4 KiB window of its own: pieces queue in the wave's
+// chunks (a span of fewer than 256 chunks is all piece, head included).  A
+// piece does not get a 4 KiB window of its own: pieces queue in the wave's
 // piece ring and one wave iteration checksums as many of them as fit in its
 // 64 lanes -- a piece takes nl = ceil((r + x) / 4) lanes, x = 1 when it needs
 // its aux chunk (the 16 bytes holding its tail word) -- each lane a 64-byte
@@ -106,16 +101,8 @@ struct Plan {
   uint32_t hp, ws, k, jv;
   uint32_t pw;    // the piece word (0: no piece)
   uint32_t seg_aux;  // m > 0, no piece, a tail: the last segment reads the aux chunk at c0 + 16 C - 12
-  uint32_t front;    // a partial first segment: its window chunks in front of chunk 0 (m counts it)
   bool empty;     // a CRC span of 0 bytes: out = init, nothing read
 };
-
-// Piece chunks from which a span's remainder runs as a partial first
-// segment instead of a back piece.
-#ifndef WIPDB_LP_PARTIAL_MIN
-#define WIPDB_LP_PARTIAL_MIN 160
-#endif
-constexpr uint32_t kPartialMin = WIPDB_LP_PARTIAL_MIN;
 
 // s_lo: the low 32 bits of the span's absolute address (sbase + a).
 WIPDB_LK_HD inline Plan MakePlan(uint64_t a, uint32_t s_lo, uint32_t n, bool verify) {
@@ -147,7 +134,6 @@ WIPDB_LK_HD inline Plan MakePlan(uint64_t a, uint32_t s_lo, uint32_t n, bool ver
   p.jv = jv;
   p.empty = !verify && n == 0u;
   p.seg_aux = 0;
-  p.front = 0;
   const uint32_t r = C & 255u;
   p.p0 = p.c0 + 4096u * static_cast<uint64_t>(p.m);
   p.pw = 0;
@@ -156,13 +142,6 @@ WIPDB_LK_HD inline Plan MakePlan(uint64_t a, uint32_t s_lo, uint32_t n, bool ver
     return p;
   }
   if (p.empty) return p;
-  if (r >= kPartialMin) {
-    p.front = 256u - r;
-    p.m += 1u;
-    p.p0 = p.c0 + 16u * static_cast<uint64_t>(C);  // the grid end
-    p.seg_aux = k != 0u ? 1u : 0u;
-    return p;
-  }
   // the piece: the whole span (m = 0, head included) or the chunks after
   // the segments (no head).  x: its aux chunk, the 16 bytes ending at the
   // 4-byte word that holds the span's last byte -- or, when those would
@@ -182,13 +161,6 @@ WIPDB_LK_HD inline Plan MakePlan(uint64_t a, uint32_t s_lo, uint32_t n, bool ver
   p.pw = PackPW(r, x, whole ? hp : 0u, whole ? ws : 0u, te, k, jv);
   return p;
 }
-
-// ---- the kernels' piece word of a plan: the piece word, or for a partial
-// first segment kPWPartial | front (such a plan has no piece) ----
-constexpr uint32_t kPWPartial = 1u << 31;
-WIPDB_LK_HD inline uint32_t PlanPW(const Plan& p) { return p.front ? (kPWPartial | p.front) : p.pw; }
-WIPDB_LK_HD inline bool PW_piece(uint32_t w) { return w != 0u && !(w & kPWPartial); }
-WIPDB_LK_HD inline uint32_t PW_front(uint32_t w) { return (w & kPWPartial) ? (w & 255u) : 0u; }
 
 // ---- plan word: what a wave needs of a span with segments besides its
 // address (c0 = a - hp) and piece word, packed so a desk lane hands it over
