@@ -214,6 +214,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t nstate = 0;        // next desk: 0 none, 1 loads issued, 2 loads waited for
   bool nsorted = false;       // next desk: sorted (empty spans answered)
   bool exhausted = false;
+  bool wide = true;           // the last sorted desk was all short spans: full desks
   // ---- the long span being run (taken from the desk or the queue) ----
   // (c0 = a - hp, plan word, piece word: crc32c_plan.h PackPL)
   uint64_t lc0 = 0;
@@ -252,6 +253,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       const uint32_t seen = lds_ld_sync(MiscAddr(kMiscUnit));
       const uint32_t rem = seen < ug ? ug - seen : 0u;
       size = rem >= 32u * kDesk ? kDesk : (rem >= 16u * kDesk ? kDesk / 2u : kDesk / 4u);
+      // half desks after a desk that held spans with segments (they take a
+      // wave iteration each: a full desk is a long stretch of one wave's work)
+      if (!wide && size == kDesk) size = kDesk / 2u;
       u = lds_add(MiscAddr(kMiscUnit), size);
     }
     u = uni(u);
@@ -373,6 +377,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
     nshort = static_cast<uint32_t>(ballot(live && !p.empty && p.m == 0u));
     nlong = static_cast<uint32_t>(ballot(live && !p.empty && p.m != 0u));
+    wide = nlong == 0u;
     // spans of kEagerSegs segments or more go to the queue right away (if it
     // has room): the workgroup's waves take them one at a time, as they
     // become free -- a desk of long spans is not left on one wave
