@@ -204,7 +204,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // ---- the desk (lanes 0 .. kDesk - 1) and the next desk, loading ----
   uint64_t da = 0, na = 0;
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
-  uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words (switch_desk)
+  uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words
+  uint32_t npl = 0, npw = 0;  // the next desk's (sort_desk)
   uint32_t dbase = 0, nbase = 0;  // first unit of the desk (span_of: its span)
   uint32_t dtotal = 0;        // the desk's long spans still counted in the held count
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
@@ -375,6 +376,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
     const bool empty = live && p.empty;
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
+    npl = PackPL(p);
+    npw = p.pw;
     nshort = static_cast<uint32_t>(ballot(live && !p.empty && p.m == 0u));
     nlong = static_cast<uint32_t>(ballot(live && !p.empty && p.m != 0u));
     wide = nlong == 0u;
@@ -424,11 +427,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // The next desk becomes the desk.
   auto switch_desk = [&]() {
     if (!nsorted) sort_desk();
-    {
-      const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
-      dpl = PackPL(p);
-      dpw = p.pw;
-    }
+    dpl = npl;
+    dpw = npw;
     da = na;
     dn = src.bytes(nn);
     di = ni;
@@ -705,11 +705,19 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       bool fidle = false;
 #pragma nounroll
       for (;;) {
+        // the desk is out of spans with segments: the next desk, if it is in,
+        // sorted, and holds only spans with segments
+        if (!lvalid && dlong == 0u && dshort == 0u && nstate == 2u && nsorted && nshort == 0u &&
+            nlong != 0u && !fidle)
+          switch_desk();
         if (!lvalid && (dlong == 0u || fidle)) break;
         if (rcnt >= 62u || rlanes + ((ns.fl & kSPush) ? PW{ns.pw}.nl() : 0u) >= 64u) break;  // a batch is due
         if (stored_prev) wait_vm<1>();
         else wait_vm<0>();
         if (nstate == 1u) nstate = 2u;
+        loads_landed(na);  // (the desk loads are older than the DMA just waited for)
+        loads_landed(nn);
+        loads_landed(ni);
         const SegW c = ns;
         const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));
         uint32_t W[16];
@@ -721,6 +729,10 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         issue_seg();
         stored_prev = seg_compute(c, W, fax);
         fidle = uni(idle_w) != 0u;
+        // while the DMA flies: the next desk sorted once its loads are in,
+        // the one after it grabbed (its loads go out after this DMA)
+        if (nstate == 2u && !nsorted) sort_desk();
+        if (nstate == 0u && !exhausted) grab_desk();
       }
     }
     LP_T(t0);
