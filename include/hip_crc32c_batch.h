@@ -92,7 +92,8 @@ extern "C" {
  * a pool of 64 Ki..1 Mi parts, past which spans stay whole).  A latency
  * tool for batches of few long spans (a lone 16 MiB span: 5.6 -> 0.14 ms);
  * batches of many short spans run slower with it.  Takes precedence over
- * HCRC_SPLIT_SMALL. */
+ * HCRC_SPLIT_SMALL.  A device batch of at most 16 spans (without
+ * HCRC_SPLIT_SMALL) takes it by itself: there one long span is the job. */
 #define HCRC_SPLIT_LONG 0x8
 
 typedef struct hcrc_ctx hcrc_ctx;

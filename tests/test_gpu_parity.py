@@ -327,12 +327,40 @@ def test_device_batch_split_long(engine, oracle):
     out = engine.batch_device(big, _t(bo), _t(bl), split_long=True)
     host_tail = big[-(1 << 20):].cpu().numpy()
     want_small = oracle.batch(host_tail, bo[1:] - np.uint64(nbig - host_tail.size), bl[1:])
-    ref_big = engine.batch_device(big, _t(bo[:1]), _t(bl[:1]))  # the unsplit kernel's answer
+    # the spans kernel's answer (17 spans: past the automatic split of tiny
+    # device batches; the 16 empty ones just return their init)
+    pad_o = np.concatenate([bo[:1], np.zeros(16, np.uint64)])
+    pad_l = np.concatenate([bl[:1], np.zeros(16, np.uint32)])
+    ref_big = engine.batch_device(big, _t(pad_o), _t(pad_l))
     got = _u32(out)
     assert int(got[1]) == int(want_small[0])
     assert int(got[0]) == int(_u32(ref_big)[0])
     del big
     torch.cuda.synchronize()
+
+
+def test_tiny_device_batches_split_long_spans_by_themselves(engine, oracle):
+    """A device batch of at most 16 spans takes the long-span split without
+    the flag (hcrc_api.cc kAutoLongSpans: a lone long span would otherwise
+    run chained on one wave): lone spans of 1 MiB + 3, 3 MiB + 5 and 128 KiB
+    (the cut), 16 mixed spans with inits and masking, 17 spans (the plain
+    spans kernel) -- against the oracle."""
+    rng = np.random.default_rng(17)
+    buf = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    d_buf = _t(buf)
+    for n in ((1 << 20) + 3, (3 << 20) + 5, 128 << 10, (128 << 10) - 1):
+        o, ln = np.array([11], np.uint64), np.array([n], np.uint32)
+        np.testing.assert_array_equal(_u32(engine.batch_device(d_buf, _t(o), _t(ln))),
+                                      oracle.batch(buf, o, ln))
+    for cnt in (16, 17):
+        lens = rng.integers(0, 600 << 10, cnt).astype(np.uint32)
+        lens[::5] = rng.integers(0, 5000, lens[::5].size)
+        offs = np.array([int(rng.integers(0, buf.size - int(n) - 1)) for n in lens], np.uint64)
+        inits = rng.integers(0, 2**32, size=cnt, dtype=np.uint64).astype(np.uint32)
+        want = oracle.batch(buf, offs, lens, inits)
+        out = engine.batch_device(d_buf, _t(offs), _t(lens), _t(inits), mask_output=True)
+        np.testing.assert_array_equal(
+            _u32(out), np.array([oracle.lib.oracle_mask(int(x)) for x in want], np.uint32))
 
 
 def test_ctx_shared_is_idempotent_per_device():

@@ -459,11 +459,20 @@ int LaunchLong(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const ui
   return rc;
 }
 
+// A device batch of at most this many spans takes the long-span split by
+// itself: its lengths are unknown on the host, and with so few spans one
+// long span is the whole job -- run whole, a span's segments are chained on
+// one wave (a lone 1 MiB span: 0.4 ms), split they run on the whole chip
+// (0.07 ms).  Larger batches keep every wave busy with spans of their own
+// (the spans kernel shares long spans over a workgroup's waves).
+constexpr size_t kAutoLongSpans = 16;
+
 // Descriptor batch on device memory, enqueued on st.
 int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
                 const uint32_t* init, uint32_t* out, size_t count, int flags, hipStream_t st) {
   const bool mask = (flags & HCRC_MASK_OUTPUT) != 0;
-  const bool split_long = (flags & HCRC_SPLIT_LONG) != 0;
+  const bool split_long = (flags & HCRC_SPLIT_LONG) != 0 ||
+                          ((flags & HCRC_SPLIT_SMALL) == 0 && count <= kAutoLongSpans);
   const bool split = !split_long && (flags & HCRC_SPLIT_SMALL) != 0;
   const size_t piece_max = split_long ? size_t(lk::kMaxListSpans) - kDevPartCap
                            : split    ? size_t(lk::kMaxListSpans)
