@@ -714,10 +714,15 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         if (rcnt >= 62u || rlanes + ((ns.fl & kSPush) ? PW{ns.pw}.nl() : 0u) >= 64u) break;  // a batch is due
         if (stored_prev) wait_vm<1>();
         else wait_vm<0>();
-        if (nstate == 1u) nstate = 2u;
-        loads_landed(na);  // (the desk loads are older than the DMA just waited for)
-        loads_landed(nn);
-        loads_landed(ni);
+        if (nstate == 1u) {
+          // the desk loads are older than the DMA just waited for: the
+          // compiler's own wait for them goes here, once per desk (not on
+          // every iteration, where it would also wait for the last store)
+          nstate = 2u;
+          loads_landed(na);
+          loads_landed(nn);
+          loads_landed(ni);
+        }
         const SegW c = ns;
         const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));
         uint32_t W[16];
@@ -725,14 +730,17 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         u32x4 fax{0, 0, 0, 0};
         if (c.fl & kSAux) fax = lds_ld4(SegAuxAddr(w));
         pp.release();
+        // the next desk sorted once its loads are in (before this
+        // iteration's DMA: any wait the compiler adds for them is free here)
+        if (nstate == 2u && !nsorted) sort_desk();
+        // the desk after the next: its loads go out BEFORE this iteration's
+        // DMA, so the wait for that DMA covers them (and the store issued
+        // after it may stay in flight)
+        if (nstate == 0u && !exhausted) grab_desk();
         if (!lvalid) take_own();
         issue_seg();
         stored_prev = seg_compute(c, W, fax);
         fidle = uni(idle_w) != 0u;
-        // while the DMA flies: the next desk sorted once its loads are in,
-        // the one after it grabbed (its loads go out after this DMA)
-        if (nstate == 2u && !nsorted) sort_desk();
-        if (nstate == 0u && !exhausted) grab_desk();
       }
     }
     LP_T(t0);
@@ -742,7 +750,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (have) {
       if (stored_prev) wait_vm<1>();
       else wait_vm<0>();
-      if (nstate == 1u) nstate = 2u;  // the next desk's loads are in
+      if (nstate == 1u) {  // the next desk's loads are in (see the segment loop)
+        nstate = 2u;
+        loads_landed(na);
+        loads_landed(nn);
+        loads_landed(ni);
+      }
       ck = nk;
       cs = ns;
       cb_pw = nb_pw;
@@ -773,10 +786,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       ck = kWNone;
     }
     const uint32_t ckind = ck & 3u;
-    // (no path into decide carries a desk load in flight: see loads_landed)
-    loads_landed(na);
-    loads_landed(nn);
-    loads_landed(ni);
+    // the next desk sorted once its loads are in (before the next DMA)
+    if (nstate == 2u && !nsorted) sort_desk();
+    // the next desk's descriptor loads go out before the next DMA (decide):
+    // the wait for that DMA covers them, the store after it may stay in
+    // flight (decide stalls on them only when the desk in hand runs dry)
+    if (nstate == 0u && !exhausted) grab_desk();
     LP_T(t1);
     decide();
     LP_T(t2);
@@ -851,16 +866,10 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     stored_prev = did_store;
     LP_T(t3);
     if (have) {
-      // while the DMA flies: queue the next desk's long spans once it is in,
-      // and take the next long span when this one is about to end (not
-      // earlier: another wave may be idle)
-      if (nstate == 2u && !nsorted) sort_desk();
+      // while the DMA flies: share the long spans this wave holds when
+      // another wave is out of work
       if (idle != 0u && (dlong | nlong) != 0u) share();
     }
-    // the next desk's descriptor loads go out after this iteration's DMA and
-    // store: the wait for that DMA covers them (nothing in decide waits on
-    // them with the next DMA not yet issued)
-    if (nstate == 0u && !exhausted) grab_desk();
     LP_T(t4);
     LP_ACC(0, t1 - t0);
     LP_ACC(1, t2 - t1);
