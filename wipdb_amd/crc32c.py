@@ -197,7 +197,8 @@ class Engine:
         """Asynchronous batch on device tensors; returns the uint32 out tensor
         (int32 storage).  Enqueued on ``stream`` (default: torch's current).
         ``split_small``: HCRC_SPLIT_SMALL (the size classes); ``split_long``:
-        HCRC_SPLIT_LONG (spans of >= 128 KiB in 16 KiB parts on many waves).  Offsets are
+        HCRC_SPLIT_LONG (spans of >= 128 KiB in 16 KiB parts on many waves;
+        batches of at most 16 spans take it by themselves).  Offsets are
         int64, lengths / inits / out 32-bit, all contiguous on this engine's
         device; ``check_bounds`` also checks every span against base (a
         device kernel and a sync, hcrc_check_spans)."""
