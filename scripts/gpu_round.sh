@@ -29,7 +29,9 @@ for s in $STEPS; do
     benchq) run benchq 200 python bench.py --steps 50 --no-cpu-baseline ;;
     extra) run extra 400 python scripts/bench_extra.py --what mixed,tblocks,vtblocks,verify ;;
     mixed) run mixed 300 python scripts/bench_extra.py --what mixed ;;
-    host) run host 400 python scripts/bench_extra.py --what sst,host4k ;;
+    host) run host 400 python scripts/bench_extra.py --what sst,sstpin,host4k ;;
+    long) run long 300 python scripts/long_span_probe.py ;;
+    cfg4) run cfg4 400 python bench.py --blocks 8388608 --steps 10 --warmup 5 ;;
     ab) run ab 900 bash scripts/gpu_abn.sh ${AB_ROUNDS:-2} ${AB_WHAT:-mixed,tblocks,vtblocks,verify} tree ${AB_LIBS:-build/ab/lib_r02.so} ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${P}_pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
