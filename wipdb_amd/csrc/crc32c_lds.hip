@@ -705,8 +705,10 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       bool fidle = false;
 #pragma nounroll
       for (;;) {
-        // the desk is out of spans with segments: the next desk, if it is in,
-        // sorted, and holds only spans with segments
+        // the desk is out of spans with segments: a span queued for the
+        // workgroup, else the next desk if it is in, sorted, and holds only
+        // spans with segments
+        if (!lvalid && dlong == 0u) pop();
         if (!lvalid && dlong == 0u && dshort == 0u && nstate == 2u && nsorted && nshort == 0u &&
             nlong != 0u && !fidle)
           switch_desk();
