@@ -637,7 +637,9 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         // (one register assignment of W whichever branch ran)
         uint32_t h4[4] = {W[0], W[1], W[2], W[3]};
         if (c.fl & kSFirst) {
-          const uint32_t inj = head_register(l, c.init, hp);
+          // (no head bytes and init 0 -- aligned blocks, WriteRawBlock's
+          // spans: ~0, no table read in front of the scan)
+          const uint32_t inj = (c.init | hp) == 0u ? ~0u : head_register(l, c.init, hp);
           if ((hp | ws) == 0u) h4[0] ^= inj;
           else fix_head(h4, hp, ws, inj);
         } else {
