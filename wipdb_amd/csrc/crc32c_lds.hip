@@ -206,8 +206,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t dn = 0, di = 0, nn = 0, ni = 0;
   uint32_t dpl = 0, dpw = 0;  // the desk's plan and piece words
   uint32_t npl = 0, npw = 0;  // the next desk's (sort_desk)
-  uint32_t dsimple = 0, nsimple = 0;  // desk lanes whose span is SIMPLE: one full segment, no
-                                      // head bytes, no tail, no piece, init 0 (the simple loop)
   uint32_t dbase = 0, nbase = 0;  // first unit of the desk (span_of: its span)
   uint32_t dtotal = 0;        // the desk's long spans still counted in the held count
   uint32_t dshort = 0;        // desk lanes whose short span is not in the ring yet
@@ -380,8 +378,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
     npl = PackPL(p);
     npw = p.pw;
-    nsimple = static_cast<uint32_t>(ballot(live && !p.empty && p.m == 1u && p.pw == 0u && p.seg_aux == 0u &&
-                                           (p.hp | p.ws | p.k | p.jv) == 0u && ni == 0u));
     nshort = static_cast<uint32_t>(ballot(live && !p.empty && p.m == 0u));
     nlong = static_cast<uint32_t>(ballot(live && !p.empty && p.m != 0u));
     wide = nlong == 0u;
@@ -433,7 +429,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (!nsorted) sort_desk();
     dpl = npl;
     dpw = npw;
-    dsimple = nsimple;
     da = na;
     dn = src.bytes(nn);
     di = ni;
@@ -712,54 +707,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       bool fidle = false;
 #pragma nounroll
       for (;;) {
-        // ---- simple spans back to back (aligned 4 KiB blocks, verify
-        // blocks of 4096 bytes on disk): a loop with nothing else live --
-        // entered with a simple span issued, left with one issued ----
-#pragma nounroll
-        while (ns.fl == (kSFirst | kSLast) && ns.hw == 0u && ns.init == 0u && dlong != 0u && !fidle &&
-               !(nstate == 2u && !nsorted) &&
-               ((dsimple >> static_cast<uint32_t>(__builtin_ctz(dlong))) & 1u) != 0u) {
-          if (stored_prev) wait_vm<1>();
-          else wait_vm<0>();
-          if (nstate == 1u) {
-            nstate = 2u;
-            loads_landed(na);
-            loads_landed(nn);
-            loads_landed(ni);
-          }
-          const uint32_t cid = ns.id;
-          const uint32_t sidle = lds_ld_sync(MiscAddr(kMiscIdle));
-          uint32_t W[16];
-          pp.read(W);
-          pp.release();
-          // the next: the desk's next (simple) span, its one segment
-          const uint32_t k = static_cast<uint32_t>(__builtin_ctz(dlong));
-          const uint64_t a = (static_cast<uint64_t>(rdlane(static_cast<uint32_t>(da >> 32), k)) << 32) |
-                             rdlane(static_cast<uint32_t>(da), k);
-          ns.id = static_cast<uint32_t>(span_of(dbase + k));
-          dlong &= dlong - 1u;
-          if (dlong == 0u) {
-            if (l == 0u) lds_add(MiscAddr(kMiscHeld), 0u - dtotal);
-            dtotal = 0;
-          }
-          const uint32_t o = 16u * pp.cm;
-          dma4(sbase + a, pp.slot, o, o + 1024u, o + 2048u, o + 3072u);
-          // the current: init 0 and no head bytes, so ~0 enters at its first word
-          W[0] ^= l == 0u ? ~0u : 0u;
-          if (kV) {
-            uint32_t lo = W[14], hi = W[15];
-            fix_trailer(lo, hi, 0u);
-            W[14] = l == 63u ? lo : W[14];
-            W[15] = l == 63u ? hi : W[15];
-          }
-          const uint32_t R = fold<1>(lk, l, scan(lk, W))[0];
-          if (l == 0u) {
-            if (kV) out8[cid] = R == residue_of(0u) ? 1u : 0u;
-            else out32[cid] = msk ? mask_crc(~R) : ~R;
-          }
-          stored_prev = true;
-          fidle = uni(sidle) != 0u;
-        }
         // the desk is out of spans with segments: a span queued for the
         // workgroup, else the next desk if it is in, sorted, and holds only
         // spans with segments
