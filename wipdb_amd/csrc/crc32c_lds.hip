@@ -54,12 +54,6 @@ namespace lk {
 // ---------------------------------------------------------------------------
 // Spans per desk (lanes 0 .. kDesk - 1 hold a desk; masks are 32 bits)
 constexpr uint32_t kDesk = 32;
-// Desks in rounds of 16, desk lanes 16 units apart (grab_desk); 0: a desk
-// holds consecutive units (an A/B build)
-#ifndef WIPDB_LP_ROUND_DESKS
-#define WIPDB_LP_ROUND_DESKS 1
-#endif
-constexpr uint32_t kLaneUnits = WIPDB_LP_ROUND_DESKS ? 16u : 1u;
 // Spans of this many segments or more are queued for the workgroup as soon
 // as their desk is sorted
 #ifndef WIPDB_LP_EAGER_SEGS
@@ -255,26 +249,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // 1; waited for at first use).  kDesk units while the workgroup has
   // plenty left, then 16 and 8 (the waves' last desks end close together).
   auto grab_desk = [&]() {
-#if WIPDB_LP_ROUND_DESKS
-    // Desks in ROUNDS of 16 (one per wave): desk i of round r holds units
-    // 512 r + i + 16 j (lane j), so the 16 desks in flight at once in a
-    // workgroup read one 16-span block at a time -- and, with the blocks
-    // round robin over the grid, the whole chip one compact window -- as
-    // round 2's per-span counter did.  The last round's units are spread
-    // over all 16 desks (its waves finish together).
-    uint32_t dn0 = 0;
-    if (l == 0u) dn0 = lds_add(MiscAddr(kMiscUnit), 1u);
-    dn0 = uni(dn0);
-    const uint32_t u = (dn0 >> 4) * (16u * kDesk) + (dn0 & 15u);
-    nbase = u;
-    if (u >= ug) {
-      exhausted = true;
-      nstate = 0;
-      return;
-    }
-    const uint32_t un = u + kLaneUnits * l;
-    const bool v = l < kDesk && un < ug;
-#else
     uint32_t u = 0, size = kDesk;
     if (l == 0u) {
       const uint32_t seen = lds_ld_sync(MiscAddr(kMiscUnit));
@@ -295,7 +269,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     }
     const uint32_t un = u + l;
     const bool v = l < size && un < ug;
-#endif
     nlive = static_cast<uint32_t>(ballot(v));
     if (v) src.lane(span_of(un), na, nn, ni);
     if (l == 0u) lds_add(MiscAddr(kMiscDesks), 1u);
@@ -388,7 +361,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       lds_st_sync(MiscAddr(kMiscQInit + (qk & (kQSlots - 1u))), iv);
     }
     lgkm_wait();  // the record before its marker
-    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(span_of(base + kLaneUnits * l)) + 1u);
+    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(span_of(base + l)) + 1u);
     if (l == 0u && held != 0u) lds_add(MiscAddr(kMiscHeld), 0u - held);  // (after the records: in order)
     return true;
   };
@@ -399,7 +372,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // the in-flight count).
   auto sort_desk = [&]() {
     const bool live = l < kDesk && ((nlive >> (l & (kDesk - 1u))) & 1u) != 0u;
-    const uint64_t s = span_of(nbase + kLaneUnits * l);
+    const uint64_t s = span_of(nbase + l);
     const Plan p = MakePlan(na, static_cast<uint32_t>(sbase + na), src.bytes(nn), kV);
     const bool empty = live && p.empty;
     if (!kV && empty) out32[s] = msk ? mask_crc(ni) : ni;
@@ -442,7 +415,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     lpl = pl;
     lpw = rdlane(dpw, k);
     linit = rdlane(di, k);
-    lid = static_cast<uint32_t>(span_of(dbase + kLaneUnits * k));
+    lid = static_cast<uint32_t>(span_of(dbase + k));
     lt = 0;
     lvalid = true;
     dlong &= dlong - 1u;
@@ -492,7 +465,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t v_lo = bperm(static_cast<uint32_t>(p0), pos);
     const uint32_t v_hi = bperm(static_cast<uint32_t>(p0 >> 32), pos);
     const uint32_t v_pw = bperm(dpw, pos), v_inj = bperm(inj, pos);
-    const uint32_t v_id = static_cast<uint32_t>(span_of(dbase + kLaneUnits * pos));
+    const uint32_t v_id = static_cast<uint32_t>(span_of(dbase + pos));
     rp_lo = me ? v_lo : rp_lo;
     rp_hi = me ? v_hi : rp_hi;
     rpw = me ? v_pw : rpw;
