@@ -54,6 +54,11 @@ namespace lk {
 // ---------------------------------------------------------------------------
 // Spans per desk (lanes 0 .. kDesk - 1 hold a desk; masks are 32 bits)
 constexpr uint32_t kDesk = 32;
+// Desk size after a desk that held spans with segments
+#ifndef WIPDB_LP_LONG_DESK
+#define WIPDB_LP_LONG_DESK 16
+#endif
+constexpr uint32_t kLongDesk = WIPDB_LP_LONG_DESK;
 // Spans of this many segments or more are queued for the workgroup as soon
 // as their desk is sorted
 #ifndef WIPDB_LP_EAGER_SEGS
@@ -256,7 +261,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       size = rem >= 32u * kDesk ? kDesk : (rem >= 16u * kDesk ? kDesk / 2u : kDesk / 4u);
       // half desks after a desk that held spans with segments (they take a
       // wave iteration each: a full desk is a long stretch of one wave's work)
-      if (!wide && size == kDesk) size = kDesk / 2u;
+      if (!wide && size > kLongDesk) size = kLongDesk;
       u = lds_add(MiscAddr(kMiscUnit), size);
     }
     u = uni(u);
