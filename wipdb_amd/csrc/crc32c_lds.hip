@@ -54,9 +54,11 @@ namespace lk {
 // ---------------------------------------------------------------------------
 // Spans per desk (lanes 0 .. kDesk - 1 hold a desk; masks are 32 bits)
 constexpr uint32_t kDesk = 32;
-// Desk size after a desk that held spans with segments
+// Desk size after a desk that held spans with segments (8: 0.650 ms on the
+// headline vs 0.658 with 16, 0.664 with 32, 0.669 with 4, 0.714 with 2 --
+// profiles/r03u_long_desk_ab.log, r03v_long_desk_small_ab.log)
 #ifndef WIPDB_LP_LONG_DESK
-#define WIPDB_LP_LONG_DESK 16
+#define WIPDB_LP_LONG_DESK 8
 #endif
 constexpr uint32_t kLongDesk = WIPDB_LP_LONG_DESK;
 // Spans of this many segments or more are queued for the workgroup as soon
