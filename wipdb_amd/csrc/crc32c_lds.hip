@@ -62,9 +62,10 @@ constexpr uint32_t kDesk = 32;
 #endif
 constexpr uint32_t kLongDesk = WIPDB_LP_LONG_DESK;
 // Spans of this many segments or more are queued for the workgroup as soon
-// as their desk is sorted
+// as their desk is sorted (8: config 3's Zipf mix +2 % over 4, same session,
+// profiles/r03w_eager_ab.log)
 #ifndef WIPDB_LP_EAGER_SEGS
-#define WIPDB_LP_EAGER_SEGS 4
+#define WIPDB_LP_EAGER_SEGS 8
 #endif
 constexpr uint32_t kEagerSegs = WIPDB_LP_EAGER_SEGS;
 
