@@ -150,6 +150,8 @@ inline uint32_t group_id() { return emu::t_bid; }
 inline uint32_t group_count() { return emu::t_grid; }
 inline void wg_sync() { emu::t_group->bar.wait(); }
 inline void lk_sleep() { std::this_thread::yield(); }
+template <int P>
+inline void lk_prio() {}
 inline uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
 inline uint32_t vperm(uint32_t a, uint32_t b, uint32_t sel) {
   uint32_t r = 0;

@@ -68,6 +68,13 @@ constexpr uint32_t kLongDesk = WIPDB_LP_LONG_DESK;
 #define WIPDB_LP_EAGER_SEGS 8
 #endif
 constexpr uint32_t kEagerSegs = WIPDB_LP_EAGER_SEGS;
+// Wave priority from a slot's arrival to the next DMA's issue (0: off): the
+// wave whose bytes just landed gets its next 4 KiB in flight ahead of the
+// other waves' compute
+#ifndef WIPDB_LP_PRIO
+#define WIPDB_LP_PRIO 0
+#endif
+constexpr int kPrio = WIPDB_LP_PRIO;
 
 // ---------------------------------------------------------------------------
 // Wave scans (row-local DPP steps, rows joined through readlane)
@@ -726,6 +733,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         if (rcnt >= 62u || rlanes + ((ns.fl & kSPush) ? PW{ns.pw}.nl() : 0u) >= 64u) break;  // a batch is due
         if (stored_prev) wait_vm<1>();
         else wait_vm<0>();
+        if constexpr (kPrio != 0) lk_prio<kPrio>();
         if (nstate == 1u) {
           // the desk loads are older than the DMA just waited for: the
           // compiler's own wait for them goes here, once per desk (not on
@@ -751,6 +759,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         if (nstate == 0u && !exhausted) grab_desk();
         if (!lvalid) take_own();
         issue_seg();
+        if constexpr (kPrio != 0) lk_prio<0>();
         stored_prev = seg_compute(c, W, fax);
         fidle = uni(idle_w) != 0u;
       }
@@ -762,6 +771,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (have) {
       if (stored_prev) wait_vm<1>();
       else wait_vm<0>();
+      if constexpr (kPrio != 0) lk_prio<kPrio>();
       if (nstate == 1u) {  // the next desk's loads are in (see the segment loop)
         nstate = 2u;
         loads_landed(na);
@@ -806,6 +816,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     if (nstate == 0u && !exhausted) grab_desk();
     LP_T(t1);
     decide();
+    if constexpr (kPrio != 0) lk_prio<0>();
     LP_T(t2);
 
     bool did_store = false;

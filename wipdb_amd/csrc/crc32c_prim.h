@@ -64,6 +64,10 @@ __device__ __forceinline__ uint32_t group_id() { return blockIdx.x; }
 __device__ __forceinline__ uint32_t group_count() { return gridDim.x; }
 __device__ __forceinline__ void wg_sync() { __syncthreads(); }
 __device__ __forceinline__ void lk_sleep() { __builtin_amdgcn_s_sleep(1); }
+// wave issue priority (s_setprio): the stretch from a slot's arrival to the
+// next DMA's issue runs above the other waves' compute
+template <int P>
+__device__ __forceinline__ void lk_prio() { __builtin_amdgcn_s_setprio(P); }
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
