@@ -203,6 +203,12 @@ inline uint64_t ballot(bool p) {
     return m;
   });
 }
+inline uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
+  return ((m >> emu::lane()) & 1u) ? a : b;
+}
+inline uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (sh & 31u));
+}
 inline uint32_t mbcnt_lo(uint32_t m, uint32_t acc) {
   const uint32_t l = emu::lane();
   return acc + static_cast<uint32_t>(__builtin_popcount(l < 32u ? (m & ((1u << l) - 1u)) : m));
@@ -235,6 +241,7 @@ inline void dma1nt(uint64_t base, uint32_t dst, uint32_t off) {
   emu::copy16(dst + 16u * emu::lane(), base + off);
 }
 inline void dma1v(uint64_t addr, uint32_t dst) { emu::copy16(dst + 16u * emu::lane(), addr); }
+inline void dma1v_c(uint64_t addr, uint32_t dst) { emu::copy16(dst + 16u * emu::lane(), addr); }
 // the wave's DMAs have landed: the lanes meet (each copied its chunks at issue)
 template <int N>
 inline void wait_vm() {

@@ -76,6 +76,22 @@ constexpr uint32_t kEagerSegs = WIPDB_LP_EAGER_SEGS;
 #define WIPDB_LP_PRIO 3
 #endif
 constexpr int kPrio = WIPDB_LP_PRIO;
+// Batch DMA addresses: the high words exchanged only when they differ
+// between stripes (1) or always (0)
+#ifndef WIPDB_LP_HI_UNI
+#define WIPDB_LP_HI_UNI 0
+#endif
+// The batch path's per-lane selects (the DMA's chunk sources, the tail word,
+// the head chunk's fix) as explicit v_cndmask on ballot masks (1) or as ?:
+// chains (0: hipcc lowered some into exec-masked branches; 1: config 3's
+// 512 B / 1 KiB / 2 KiB buckets +7 %, same session, profiles/r03v2_vsel_ab.log)
+#ifndef WIPDB_LP_VSEL
+#define WIPDB_LP_VSEL 1
+#endif
+// The batch DMA nontemporal (1) or through the caches (0, an A/B build)
+#ifndef WIPDB_LP_BATCH_NT
+#define WIPDB_LP_BATCH_NT 1
+#endif
 
 // ---------------------------------------------------------------------------
 // Wave scans (row-local DPP steps, rows joined through readlane)
@@ -158,6 +174,33 @@ __device__ __forceinline__ uint32_t word_at(uint32_t c0, uint32_t c1, uint32_t c
   const uint32_t lo = q == 0u ? c0 : (q == 1u ? c1 : (q == 2u ? c2 : c3));
   const uint32_t hi = q == 0u ? c1 : (q == 1u ? c2 : (q == 2u ? c3 : 0u));
   return sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
+}
+
+// word_at with the selects on ballot masks (all lanes call it)
+__device__ __forceinline__ uint32_t word_at_v(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t e) {
+  const uint32_t q = e >> 2;
+  const uint64_t q1 = ballot(q == 1u), q2 = ballot(q == 2u), q3 = ballot(q == 3u);
+  const uint32_t lo = vsel(q3, c3, vsel(q2, c2, vsel(q1, c1, c0)));
+  const uint32_t hi = vsel(q3, 0u, vsel(q2, c3, vsel(q1, c2, c1)));
+  return alignbit(hi, lo, 8u * (e & 3u));
+}
+// fix_head (crc32c_plan.h) with the selects on ballot masks and the head
+// masks by a 64-bit shift (all lanes call it; per-lane hp, ws, inj)
+__device__ __forceinline__ void fix_head_v(uint32_t (&c)[4], uint32_t hp, uint32_t ws, uint32_t inj) {
+  const uint64_t w1 = ballot(ws == 1u), w2 = ballot(ws == 2u), w3 = ballot(ws == 3u);
+  uint32_t d[4];
+  d[3] = vsel(w3, c[0], vsel(w2, c[1], vsel(w1, c[2], c[3])));
+  d[2] = vsel(w3, 0u, vsel(w2, c[0], vsel(w1, c[1], c[2])));
+  d[1] = vsel(w3 | w2, 0u, vsel(w1, c[0], c[1]));
+  d[0] = vsel(w3 | w2 | w1, 0u, c[0]);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int32_t t0 = static_cast<int32_t>(hp) - 4 * w;
+    const uint32_t t = static_cast<uint32_t>(t0 < 0 ? 0 : (t0 > 4 ? 4 : t0));
+    c[w] = d[w] & static_cast<uint32_t>(0xffffffffull << (8u * t));
+  }
+  c[0] ^= inj;
 }
 
 // A segment iteration (uniform).
@@ -557,13 +600,38 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       if (live) dma1v(a, pp.slot + 1024u * q);
     }
 #else
+#if WIPDB_LP_HI_UNI
+    // the stripes' high address words are one value when the batch's pieces
+    // lie in one 4 GiB window (lane 0 is always live): then only the low
+    // words and the stripe info travel
+    const uint32_t h0 = rdlane(s_hi, 0);
+    const bool hu = ballot(live && s_hi != h0) == 0u;
+#endif
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
       const uint32_t sl = 16u * q + dsl;
+#if WIPDB_LP_HI_UNI
+      const uint32_t x_lo = bperm(s_lo, sl), x_in = bperm(sp.info, sl);
+      uint32_t x_hi = h0;
+      if (!hu) x_hi = bperm(s_hi, sl);
+#else
       const uint32_t x_lo = bperm(s_lo, sl), x_hi = bperm(s_hi, sl), x_in = bperm(sp.info, sl);
+#endif
+#if WIPDB_LP_VSEL
+      // StripeChunkSrc(x_in, dci) on ballot masks
+      const uint32_t fr = x_in & 7u;
+      const uint64_t lt = ballot(dci < fr), eq = ballot(dci == fr && (x_in & 8u) != 0u);
+      const uint32_t off = vsel(lt, x_in >> 6, 16u * dci + vsel(eq, (x_in >> 2) & 12u, 0u));
+      const uint64_t a = ((static_cast<uint64_t>(x_hi) << 32) | x_lo) + off;
+#else
       const uint64_t a = ((static_cast<uint64_t>(x_hi) << 32) | x_lo) +
                          static_cast<uint64_t>(StripeChunkSrc(x_in, dci));
+#endif
+#if WIPDB_LP_BATCH_NT
       if (sl < used) dma1v(a, pp.slot + 1024u * q);
+#else
+      if (sl < used) dma1v_c(a, pp.slot + 1024u * q);
+#endif
     }
 #endif
     nb_pw = pw.v;
@@ -831,7 +899,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       const uint32_t j = cb_j, nl = pw.nl(), r = pw.r();
       const int32_t f = static_cast<int32_t>(pw.front()) - 4 * static_cast<int32_t>(j);
       // lane 0 of a piece with a tail: its chunk 0 is the aux chunk
+#if WIPDB_LP_VSEL
+      const uint32_t tw = word_at_v(W[0], W[1], W[2], W[3], pw.te());
+#else
       const uint32_t tw = word_at(W[0], W[1], W[2], W[3], pw.te());
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bool z = !live || i < f;
@@ -842,6 +914,19 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       if (ballot(live && r != 0u && f >= 0 && f < 4) != 0u) {
         const bool has = live && r != 0u && f >= 0 && f < 4;
         uint32_t c[4];
+#if WIPDB_LP_VSEL
+        const uint64_t f1 = ballot(f == 1), f2 = ballot(f == 2), f3 = ballot(f == 3);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          c[q] = vsel(f3, W[12 + q], vsel(f2, W[8 + q], vsel(f1, W[4 + q], W[q])));
+        fix_head_v(c, pw.hp(), pw.ws(), cb_inj);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint64_t hi = ballot(has && f == i);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) W[4 * i + q] = vsel(hi, c[q], W[4 * i + q]);
+        }
+#else
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           c[q] = f == 0 ? W[q] : (f == 1 ? W[4 + q] : (f == 2 ? W[8 + q] : W[12 + q]));
@@ -850,6 +935,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) W[4 * i + q] = has && f == i ? c[q] : W[4 * i + q];
+#endif
       }
       if (kV) {
         uint32_t lo = W[14], hi = W[15];

@@ -97,6 +97,18 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t k) {
   return __builtin_amdgcn_readlane(v, k);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// Per-lane select by a wave mask: m's bit of the lane ? a : b, one
+// v_cndmask_b32 with the mask in an SGPR pair (hipcc lowered some per-lane ?:
+// chains of the batch path into exec-masked branches)
+__device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+  return r;
+}
+// The low word of (hi:lo) >> (sh % 32) (v_alignbit_b32)
+__device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbit(hi, lo, sh);
+}
 __device__ __forceinline__ uint32_t mbcnt_lo(uint32_t m, uint32_t acc) {
   return __builtin_amdgcn_mbcnt_lo(m, acc);
 }
@@ -189,6 +201,21 @@ __device__ __forceinline__ void dma1v(uint64_t addr, uint32_t dst) {
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(addr), "s"(dst)
+      : "memory");
+}
+
+// The same through the caches (no nt): lines at span edges, shared with the
+// neighbouring span, may then hit in L2 -- an A/B build of the batch DMA.
+__device__ __forceinline__ void dma1v_c(uint64_t addr, uint32_t dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(addr), "s"(dst)
