@@ -88,6 +88,11 @@ constexpr int kPrio = WIPDB_LP_PRIO;
 #ifndef WIPDB_LP_VSEL
 #define WIPDB_LP_VSEL 1
 #endif
+// MakeStripe's per-lane select on a ballot mask too (1; no measurable
+// change, profiles/r03v3_stripe_atomicopt_ab.log: one exec-masked branch fewer)
+#ifndef WIPDB_LP_VSEL2
+#define WIPDB_LP_VSEL2 1
+#endif
 // The batch DMA nontemporal (1) or through the caches (0, an A/B build)
 #ifndef WIPDB_LP_BATCH_NT
 #define WIPDB_LP_BATCH_NT 1
@@ -201,6 +206,20 @@ __device__ __forceinline__ void fix_head_v(uint32_t (&c)[4], uint32_t hp, uint32
     c[w] = d[w] & static_cast<uint32_t>(0xffffffffull << (8u * t));
   }
   c[0] ^= inj;
+}
+
+// MakeStripe (crc32c_plan.h) with its select on a ballot mask (all lanes
+// call it)
+__device__ __forceinline__ Stripe make_stripe_v(PW pw, uint32_t j) {
+  const int32_t f = static_cast<int32_t>(pw.front()) - 4 * static_cast<int32_t>(j);
+  const uint32_t fr = f <= 0 ? 0u : static_cast<uint32_t>(f);
+  const uint32_t real0 = (f >= 0 && f < 4 && pw.r() != 0u) ? 1u : 0u;
+  Stripe st;
+  st.s = -16 * static_cast<int64_t>(f);
+  const uint32_t src = vsel(ballot(pw.x() != 0u), 16u * pw.r() - pw.te(), 4u * pw.ws());
+  const uint32_t dif = src + 16u * static_cast<uint32_t>(f);
+  st.info = fr | (real0 << 3) | (pw.ws() << 4) | (fr ? dif << 6 : 0u);
+  return st;
 }
 
 // A segment iteration (uniform).
@@ -586,7 +605,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t b_st = bperm(st, e);
     const PW pw{live ? b_pw : 0u};
     const uint32_t j = live ? pw.j0() + (l - b_st) : 0u;  // the lane's stripe of its piece
+#if WIPDB_LP_VSEL2
+    const Stripe sp = make_stripe_v(pw, j);
+#else
     const Stripe sp = MakeStripe(pw, j);
+#endif
     const uint64_t S = sbase + ((static_cast<uint64_t>(b_hi) << 32) | b_lo) +
                        static_cast<uint64_t>(sp.s);
     const uint32_t s_lo = static_cast<uint32_t>(S), s_hi = static_cast<uint32_t>(S >> 32);
