@@ -185,6 +185,18 @@ inline uint32_t dpp(uint32_t v) {
     return src < 0 ? 0u : static_cast<uint32_t>(b[src]);
   }));
 }
+inline uint32_t bcast15(uint32_t v) {
+  return static_cast<uint32_t>(emu::xchg(v, [](const uint64_t* b) -> uint64_t {
+    const int l = static_cast<int>(emu::lane()), row = l >> 4;
+    return (row == 1 || row == 3) ? static_cast<uint32_t>(b[16 * row - 1]) : 0u;
+  }));
+}
+inline uint32_t bcast31(uint32_t v) {
+  return static_cast<uint32_t>(emu::xchg(v, [](const uint64_t* b) -> uint64_t {
+    const int row = static_cast<int>(emu::lane()) >> 4;
+    return row >= 2 ? static_cast<uint32_t>(b[31]) : 0u;
+  }));
+}
 inline uint32_t uni(uint32_t v) {
   return static_cast<uint32_t>(emu::xchg(v, [](const uint64_t* b) { return b[0]; }));
 }

@@ -98,6 +98,11 @@ constexpr int kPrio = WIPDB_LP_PRIO;
 #define WIPDB_LP_BATCH_NT 1
 #endif
 
+// Wave scans: rows joined by DPP row broadcasts (1) or through readlane (0)
+#ifndef WIPDB_LP_BCAST
+#define WIPDB_LP_BCAST 0
+#endif
+
 // ---------------------------------------------------------------------------
 // Wave scans (row-local DPP steps, rows joined through readlane)
 // ---------------------------------------------------------------------------
@@ -106,6 +111,10 @@ __device__ __forceinline__ uint32_t scan_add(uint32_t v, uint32_t l) {
   v += dpp<0x112>(v);  // row_shr:2
   v += dpp<0x114>(v);  // row_shr:4
   v += dpp<0x118>(v);  // row_shr:8
+#if WIPDB_LP_BCAST
+  v += bcast15(v);     // rows joined by DPP row broadcasts
+  return v + bcast31(v);
+#endif
   const uint32_t r0 = rdlane(v, 15), r1 = rdlane(v, 31),
                  r2 = rdlane(v, 47);
   return v + (l >= 16u ? r0 : 0u) + (l >= 32u ? r1 : 0u) + (l >= 48u ? r2 : 0u);
@@ -115,6 +124,10 @@ __device__ __forceinline__ uint32_t scan_xor(uint32_t v, uint32_t l) {
   v ^= dpp<0x112>(v);
   v ^= dpp<0x114>(v);
   v ^= dpp<0x118>(v);
+#if WIPDB_LP_BCAST
+  v ^= bcast15(v);
+  return v ^ bcast31(v);
+#endif
   const uint32_t r0 = rdlane(v, 15), r1 = rdlane(v, 31),
                  r2 = rdlane(v, 47);
   return v ^ (l >= 16u ? r0 : 0u) ^ (l >= 32u ? r1 : 0u) ^ (l >= 48u ? r2 : 0u);

@@ -81,6 +81,15 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
   return static_cast<uint32_t>(
       __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, 0xF, 0xF, true));
 }
+// DPP row broadcasts: bcast15 gives rows 1 and 3 lane 15 of the row before
+// (rows 0 and 2: 0), bcast31 gives rows 2 and 3 lane 31 (rows 0 and 1: 0) --
+// the last two steps of a wave scan after the row_shr steps
+__device__ __forceinline__ uint32_t bcast15(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xA, 0xF, false));
+}
+__device__ __forceinline__ uint32_t bcast31(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xC, 0xF, false));
+}
 // uniform value of the wave (all lanes active)
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
