@@ -98,9 +98,10 @@ constexpr int kPrio = WIPDB_LP_PRIO;
 #define WIPDB_LP_BATCH_NT 1
 #endif
 
-// Wave scans: rows joined by DPP row broadcasts (1) or through readlane (0)
+// Wave scans: rows joined by DPP row broadcasts (1: short buckets and the mix
+// +0.5-1 %, same session, profiles/r03v4_bcast_ab.log) or through readlane (0)
 #ifndef WIPDB_LP_BCAST
-#define WIPDB_LP_BCAST 0
+#define WIPDB_LP_BCAST 1
 #endif
 
 // ---------------------------------------------------------------------------
