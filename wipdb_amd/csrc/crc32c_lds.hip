@@ -103,6 +103,10 @@ constexpr int kPrio = WIPDB_LP_PRIO;
 #ifndef WIPDB_LP_BCAST
 #define WIPDB_LP_BCAST 1
 #endif
+// the wave OR too (1, A/B)
+#ifndef WIPDB_LP_BCAST_OR
+#define WIPDB_LP_BCAST_OR 0
+#endif
 
 // ---------------------------------------------------------------------------
 // Wave scans (row-local DPP steps, rows joined through readlane)
@@ -138,6 +142,10 @@ __device__ __forceinline__ uint32_t scan_or(uint32_t v) {  // the OR of the wave
   v |= dpp<0x112>(v);
   v |= dpp<0x114>(v);
   v |= dpp<0x118>(v);
+#if WIPDB_LP_BCAST_OR
+  v |= bcast15(v);
+  return rdlane(v | bcast31(v), 63);
+#endif
   return rdlane(v, 15) | rdlane(v, 31) |
          rdlane(v, 47) | rdlane(v, 63);
 }
