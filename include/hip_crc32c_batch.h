@@ -71,6 +71,8 @@ extern "C" {
 #define HCRC_ERR_LAUNCH (-5)    /* kernel launch failed                  */
 #define HCRC_ERR_MISMATCH (-6)  /* hcrc_verify*: at least one bad block  */
 #define HCRC_ERR_BOUNDS (-7)    /* hcrc_check_spans: a span leaves base   */
+#define HCRC_ERR_KERNEL (-8)    /* a kernel reported an internal fault:   */
+                                /* some outputs were not written          */
 
 /* flags */
 #define HCRC_HOST_PTRS 0x0    /* all array/data pointers are host memory    */
@@ -171,7 +173,22 @@ int hcrc_check_spans(hcrc_ctx* ctx, uint64_t base_bytes,
                      const uint64_t* d_offsets, const uint32_t* d_lengths,
                      uint32_t extra, size_t count, uint64_t* first_bad);
 
-/* Wait for all work on `stream` (NULL = the HIP default stream). */
+/* In-kernel faults.  The lane-packed kernels never leave a span
+ * uncomputed without saying so: a wait of the workgroup's long-span queue
+ * that runs out of its bound (no schedule of a resident workgroup gets
+ * there) sets a fault word instead.  The synchronous entry points
+ * (hcrc_batch, hcrc_batch_multi*) check their own word and return
+ * HCRC_ERR_KERNEL (outputs incomplete; the C++ ExtendBatch(kAuto) then
+ * computes the batch on the CPU).  Launches on a caller's stream (the
+ * *_async entry points) share the context's word: hcrc_ctx_check returns
+ * HCRC_ERR_KERNEL if any of them reported a fault since the last check
+ * (and clears it) -- call it after synchronising those streams.  The
+ * reference's Extend is infallible (kv/src/util/crc32c.h:24); a wrong CRC
+ * returned as success is the one failure a checksum must never have. */
+int hcrc_ctx_check(hcrc_ctx* ctx);
+
+/* Wait for all work on `stream` (NULL = the HIP default stream), then
+ * hcrc_ctx_check. */
 int hcrc_sync(hcrc_ctx* ctx, void* stream);
 
 /* Host-memory batch sharded over `ndev` devices by bytes, one host thread

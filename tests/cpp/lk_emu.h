@@ -144,6 +144,22 @@ template <class T>
 inline void loads_landed(T&) {}
 inline uint32_t vzero() { return 0u; }
 
+// ---- faults ----
+// the fault bits of the launches (the device counts faulting waves instead)
+namespace emu {
+inline std::atomic<uint32_t> g_faults{0};
+}
+inline void report_fault(uint32_t bits) {
+  if (emu::lane() == 0u) emu::g_faults.fetch_or(bits);
+}
+// queue record g_hide_marker's marker reads as 0 (never written): forces the
+// popper's timeout (with a small WIPDB_LP_SPIN)
+namespace emu {
+inline std::atomic<uint32_t> g_hide_marker{~0u};
+inline std::atomic<uint32_t> g_spin{1u << 22};  // WIPDB_LP_SPIN of the emulation
+}
+inline uint32_t queue_marker(uint32_t v, uint32_t idx) { return idx == emu::g_hide_marker.load() ? 0u : v; }
+
 // ---- lanes ----
 inline uint32_t lane_tid() { return emu::t_tid; }
 inline uint32_t group_id() { return emu::t_bid; }

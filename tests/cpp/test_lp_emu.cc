@@ -7,9 +7,13 @@
 // with good and corrupted trailers, and every DMA source inside the test's
 // buffer.  Catches control-flow and indexing errors of the kernel loop (the
 // desk, the ring, the queue, the batch packing) before a GPU run.
+// The queue's timeout path is forced once (a hidden record marker and a small
+// spin bound): the launch must report the fault.
 // Build: clang++ -std=c++17 -O1 -pthread -I wipdb_amd/csrc -I tests/cpp.
 // Usage: test_lp_emu [case ...]; exit 0 = pass.
 #define WIPDB_LK_EMU 1
+// the queue's spin bound, set per case (run-time in the emulation)
+#define WIPDB_LP_SPIN (::wipdb::lk::emu::g_spin.load())
 #include "crc32c_lds.hip"
 
 #include <stdio.h>
@@ -61,8 +65,10 @@ void Report(const char* name, const std::vector<uint32_t>& got, const std::vecto
   }
   const uint64_t bs = emu::g_bad_src.exchange(0);
   if (bs) fprintf(stderr, "  %s: DMA source %#llx outside the buffer\n", name, (unsigned long long)(bs & ~1ull));
-  printf("%-34s %6zu spans  %s (%zu bad)\n", name, want.size(), bad || bs ? "FAIL" : "ok", bad);
-  if (bad || bs) ++g_fail;
+  const uint32_t fb = emu::g_faults.exchange(0);
+  if (fb) fprintf(stderr, "  %s: the launch reported fault bits %#x\n", name, fb);
+  printf("%-34s %6zu spans  %s (%zu bad)\n", name, want.size(), bad || bs || fb ? "FAIL" : "ok", bad);
+  if (bad || bs || fb) ++g_fail;
 }
 
 // CRC batch through crc32c_lds_spans_kernel
@@ -234,6 +240,35 @@ int main(int argc, char** argv) {
     auto l = lens_of(700, 16384, 24000);
     auto in = inits_of(l.size());
     RunSpans("queue full: 700 long (inits)", buf, Packed(l, 7, 5), l, &in, false, 1);
+  }
+  if (Want(argc, argv, "queue timeout")) {
+    // record 0's marker hidden, a bound of 64 spins: its popper times out.
+    // The launch must end (no hang), say so in its error word (kFaultQueuePop;
+    // slot 0 then stays claimed, so record 256's producer reports
+    // kFaultQueueSlot rather than overwrite it), and every span it did not
+    // lose must still be right.
+    auto l = lens_of(700, 16384, 24000);
+    const auto o = Packed(l, 7, 5);
+    std::vector<uint32_t> want(l.size()), got(l.size(), 0x5A5A5A5Au);
+    for (size_t i = 0; i < l.size(); ++i) want[i] = Extend(0u, buf.data() + o[i], l[i]);
+    SetRange(buf);
+    emu::g_spin = 64;
+    emu::g_hide_marker = 0;
+    const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
+    emu::launch(1, [&] {
+      crc32c_lds_spans_kernel<0>(buf.data(), o.data(), l.data(), nullptr, got.data(), l.size(), 0u,
+                                 img);
+    });
+    emu::g_spin = 1u << 22;
+    emu::g_hide_marker = ~0u;
+    size_t lost = 0;
+    for (size_t i = 0; i < l.size(); ++i) lost += got[i] != want[i];
+    const uint32_t fb = emu::g_faults.exchange(0);
+    const bool ok = (fb & kFaultQueuePop) != 0 && lost >= 1 && lost <= 4 &&
+                    emu::g_bad_src.exchange(0) == 0;
+    printf("%-34s %6zu spans  %s (fault bits %#x, %zu lost)\n", "queue timeout: fault reported",
+           l.size(), ok ? "ok" : "FAIL", fb, lost);
+    if (!ok) ++g_fail;
   }
   if (Want(argc, argv, "zipf mix")) {
     const uint32_t B[] = {512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};

@@ -4,7 +4,7 @@
 // rocksdb/util/crc32c_test.cc:66-138 and leveldb/util/crc32c_test.cc:13-66
 // for both namespaces, then exercises ExtendBatch.
 //
-// Usage: test_surface [expect_gpu]   (exit 0 = pass)
+// Usage: test_surface [mode]   (exit 0 = pass; modes in main)
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -63,7 +63,8 @@ static uint32_t RdbUnmask(uint32_t c) { return rocksdb::crc32c::Unmask(c); }
 
 int main(int argc, char** argv) {
   // argv[1]: 0 = no device, 1 = a device, 2 = a device + WIPDB_CRC_MODE=cpu,
-  // 3 = a device + WIPDB_CRC_DEVICES=0,0
+  // 3 = a device + WIPDB_CRC_DEVICES=0,0, 4 = a device, linked against the
+  // test build with WIPDB_HCRC_FORCE_FAULT=1 (every kernel reports a fault)
   const int mode = argc > 1 ? atoi(argv[1]) : 0;
   const bool expect_gpu = mode != 0;
   StandardResults<KvExtend, KvMask, KvUnmask>();
@@ -103,7 +104,16 @@ int main(int argc, char** argv) {
            0);
   for (size_t i = 0; i < off.size(); ++i) CHECK_EQ(got[i], want[i]);
   auto st = wipdb::crc32c::GetBatchStats();
-  if (mode == 2) {
+  if (mode == 4) {
+    // the kernel reported a fault: kAuto computed the batch on the host
+    // (outputs right, checked above), kGpuOnly returns HCRC_ERR_KERNEL
+    CHECK_EQ(st.cpu_batches, 2);
+    CHECK_EQ(st.gpu_batches, 0);
+    CHECK_EQ(st.last_error, HCRC_ERR_KERNEL);
+    CHECK_EQ(wipdb::crc32c::ExtendBatch(file.data(), off.data(), len.data(), nullptr,
+                                        got.data(), off.size(), true, BatchPolicy::kGpuOnly),
+             HCRC_ERR_KERNEL);
+  } else if (mode == 2) {
     // GPU present, WIPDB_CRC_MODE=cpu: kAuto stays on the host, kGpuOnly
     // still reaches the device
     CHECK_EQ(st.cpu_batches, 2);

@@ -25,6 +25,7 @@ HCRC_ERR_HIP = -4
 HCRC_ERR_LAUNCH = -5
 HCRC_ERR_MISMATCH = -6
 HCRC_ERR_BOUNDS = -7
+HCRC_ERR_KERNEL = -8
 
 HCRC_HOST_PTRS = 0x0
 HCRC_DEVICE_PTRS = 0x1
@@ -55,6 +56,7 @@ _PROTOS = {
     "hcrc_verify_async": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "hcrc_verify_async_ex": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _c.c_int, _vp]),
     "hcrc_sync": (_c.c_int, [_vp, _vp]),
+    "hcrc_ctx_check": (_c.c_int, [_vp]),
     "hcrc_batch_multi": (
         _c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _vp, _vp, _vp, _vp, _vp, _sz, _c.c_int]),
     "hcrc_batch_multi_ex": (

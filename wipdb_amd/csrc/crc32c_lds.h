@@ -72,6 +72,7 @@ constexpr uint32_t kMiscDesks = 275;   // desks grabbed, not sorted yet (run_lp)
 constexpr uint32_t kMiscIdle = 276;    // waves out of work, waiting for shared long spans
 constexpr uint32_t kMiscHeld = 277;    // long spans held by a wave, not taken or shared yet
 constexpr uint32_t kMiscQRes = 278;    // queue records pushed and not yet freed (<= kQSlots)
+constexpr uint32_t kMiscFault = 279;   // kFault* bits of the workgroup (run_lp)
 constexpr uint32_t kMiscQInit = 576;   // 256 words: the init_crc of queue record k
 constexpr uint32_t kMiscBytes = 1024 * 4;
 
@@ -91,6 +92,11 @@ WIPDB_LK_HD constexpr uint32_t SegAuxAddr(uint32_t w) { return kLdsL2 + (128u + 
 
 // Flags of a launch (the HCRC_MASK_OUTPUT value is shared with the C-ABI).
 constexpr uint32_t kFlagMask = 0x2;
+// Fault bits a launch ORs into its error word (a span was left uncomputed;
+// the host returns HCRC_ERR_KERNEL): a queue record whose producer never
+// wrote it, a queue slot never freed for its next record.
+constexpr uint32_t kFaultQueuePop = 0x1;
+constexpr uint32_t kFaultQueueSlot = 0x2;
 
 // Size classes (HCRC_SPLIT_SMALL).  A span of n bytes at address a covers
 // f = (a % 16 + n) / 16 full chunks of its 16-byte grid.  Class 4 (16-lane

@@ -108,6 +108,15 @@ constexpr int kPrio = WIPDB_LP_PRIO;
 #define WIPDB_LP_BCAST_OR 0
 #endif
 
+// Bound of the long-span queue's spins (a popper waiting for its record's
+// producer, a producer waiting for a slot to be freed): never reached while
+// the workgroup's waves run (each wait is for a wave that writes next); if it
+// is, the launch reports a fault (kFault*) instead of computing a wrong CRC.
+// The host emulation sets a small bound to exercise that path.
+#ifndef WIPDB_LP_SPIN
+#define WIPDB_LP_SPIN (1u << 22)
+#endif
+
 // ---------------------------------------------------------------------------
 // Wave scans (row-local DPP steps, rows joined through readlane)
 // ---------------------------------------------------------------------------
@@ -256,6 +265,19 @@ struct SegW {
 // What an iteration computes.
 constexpr uint32_t kWNone = 0u, kWSeg = 1u, kWBatch = 2u;
 
+#if !defined(WIPDB_LK_EMU)
+// Launches of the lane-packed kernels that reported a fault (kFault*), per
+// device, ever: the host compares it before and after its launches
+// (hcrc_api.cc; wipdb_lp_fault_counter).  A module global rather than a
+// kernel argument: its address is rematerialised where the report is made,
+// so no register stays live for it through the loop.
+__device__ unsigned int g_lp_faults;
+__device__ __forceinline__ void report_fault(uint32_t) {
+  // every lane of the wave adds: the count only needs to grow
+  __hip_atomic_fetch_add(&g_lp_faults, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
+
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
 // Profiling build only: per wave, the cycles of each part of run_lp's loop
 // (s_memtime) and its iteration counts, summed over launches.
@@ -401,8 +423,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t ra = QRecAddr(idx);
     uint32_t r3 = 0;
 #pragma nounroll
-    for (uint32_t spin = 0; spin < (1u << 22); ++spin) {  // its producer writes it next
-      r3 = uni(lds_ld_sync(ra + 12u));
+    for (uint32_t spin = 0; spin < WIPDB_LP_SPIN; ++spin) {  // its producer writes it next
+      r3 = uni(queue_marker(lds_ld_sync(ra + 12u), idx));
       if (r3 != 0u) break;
       lk_sleep();
     }
@@ -412,10 +434,19 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
                    ri = uni(lds_ld_sync(MiscAddr(kMiscQInit + (idx & (kQSlots - 1u)))));
     lgkm_wait();  // read before the slot is freed
     if (l == 0u) {
-      lds_st_sync(ra + 12u, 0u);
-      lds_add(MiscAddr(kMiscQRes), 0xffffffffu);
+      if (r3 != 0u) {
+        lds_st_sync(ra + 12u, 0u);
+        lds_add(MiscAddr(kMiscQRes), 0xffffffffu);
+      } else {
+        // never written within the bound (no schedule of the workgroup's
+        // waves gets here: its producer reserved the slot and writes it
+        // next) -- the span is lost, so the launch reports it; the record
+        // stays claimed and unfreed, so no later push overwrites a slot its
+        // producer may still fill
+        lds_st_sync(MiscAddr(kMiscFault), kFaultQueuePop);
+      }
     }
-    if (r3 == 0u) return;  // never written (cannot happen; no hang if it does)
+    if (r3 == 0u) return;
     const uint64_t a = (static_cast<uint64_t>(r1) << 32) | r0;
     lid = r3 - 1u;
     linit = ri;
@@ -448,20 +479,24 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t ra = QRecAddr(qk);
     // a slot is reused only once its last record has been read (queue
     // records are popped by the waves that asked for work: this rarely waits)
+    bool busy = false;
 #pragma nounroll
-    for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
-      const bool busy = lng && lds_ld_sync(ra + 12u) != 0u;
+    for (uint32_t spin = 0; spin < WIPDB_LP_SPIN; ++spin) {
+      busy = lng && lds_ld_sync(ra + 12u) != 0u;
       if (ballot(busy) == 0u) break;
       lk_sleep();
     }
-    if (lng) {
+    // a slot still not freed within the bound is never overwritten: its span
+    // is lost (the record's popper then reports it too) and the launch says so
+    if (busy) lds_st_sync(MiscAddr(kMiscFault), kFaultQueueSlot);
+    if (lng && !busy) {
       lds_st_sync(ra, static_cast<uint32_t>(a));
       lds_st_sync(ra + 4u, static_cast<uint32_t>(a >> 32));
       lds_st_sync(ra + 8u, b);
       lds_st_sync(MiscAddr(kMiscQInit + (qk & (kQSlots - 1u))), iv);
     }
     lgkm_wait();  // the record before its marker
-    if (lng) lds_st_sync(ra + 12u, static_cast<uint32_t>(span_of(base + l)) + 1u);
+    if (lng && !busy) lds_st_sync(ra + 12u, static_cast<uint32_t>(span_of(base + l)) + 1u);
     if (l == 0u && held != 0u) lds_add(MiscAddr(kMiscHeld), 0u - held);  // (after the records: in order)
     return true;
   };
@@ -1043,6 +1078,14 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     }
     have = true;
   }
+  // a queue wait that ran out of its bound (kFault*, kept in LDS) is
+  // reported when the wave leaves: the wave that saw it leaves after it (a
+  // global write inside the queue's code made hipcc lose track of the uniform
+  // values there; a register for it cost SGPR spills)
+  {
+    const uint32_t f = uni(lds_ld_sync(MiscAddr(kMiscFault)));
+    if (f != 0u) report_fault(f);
+  }
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
   LP_T(t_end);
   prof[7] = t_end - t_start;
@@ -1094,6 +1137,25 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
 
 }  // namespace lk
 }  // namespace wipdb
+
+#if !defined(WIPDB_LK_EMU)
+// Counts one fault as a faulting wave does (the test build's
+// WIPDB_HCRC_FORCE_FAULT launches it after each lane-packed launch).
+__global__ void crc32c_lds_fault_probe_kernel() {
+  if (threadIdx.x == 0) wipdb::lk::report_fault(wipdb::lk::kFaultQueuePop);
+}
+
+// The device address of g_lp_faults on the current device (hcrc_api.cc).
+namespace wipdb {
+namespace lk {
+unsigned int* LpFaultCounter() {
+  void* p = nullptr;
+  return hipGetSymbolAddress(&p, HIP_SYMBOL(g_lp_faults)) == hipSuccess
+             ? static_cast<unsigned int*>(p) : nullptr;
+}
+}  // namespace lk
+}  // namespace wipdb
+#endif
 
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
 // Profiling build only: copies (and with reset != 0 zeroes) g_lp_prof.

@@ -58,6 +58,11 @@ __device__ __forceinline__ void loads_landed(T& v) { asm volatile("" : "+v"(v));
 // one that every later LDS access would also wait for)
 __device__ __forceinline__ uint32_t vzero() { return __builtin_amdgcn_mbcnt_lo(0u, 0u); }
 
+// ---- faults ----
+// A queue record's marker as read (the host emulation can hide one to force
+// the timeout path; here the identity).
+__device__ __forceinline__ uint32_t queue_marker(uint32_t v, uint32_t) { return v; }
+
 // ---- lanes ----
 __device__ __forceinline__ uint32_t lane_tid() { return threadIdx.x; }
 __device__ __forceinline__ uint32_t group_id() { return blockIdx.x; }

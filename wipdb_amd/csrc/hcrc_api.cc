@@ -43,6 +43,7 @@ __global__ void crc32c_lds_strided_kernel(const uint8_t*, uint64_t, uint32_t, ui
                                           uint32_t*, uint64_t, uint32_t, const uint8_t*);
 __global__ void crc32c_lds_verify_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                          uint8_t*, uint64_t, const uint8_t*);
+unsigned int* LpFaultCounter();
 template <int G, int OUT>
 __global__ void crc32c_lds_list_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                        const uint32_t*, const uint32_t*, const uint32_t*, void*,
@@ -65,6 +66,8 @@ __global__ void split_combine_kernel(const uint32_t*, const uint32_t*, const uin
                                      uint32_t, uint32_t);
 }  // namespace util
 }  // namespace wipdb
+
+__global__ void crc32c_lds_fault_probe_kernel();
 
 namespace lk = wipdb::lk;
 
@@ -202,6 +205,7 @@ struct Lane {
   hipStream_t stream = nullptr;
   Slot slots[2];
   bool slots_ready = false;
+  int index = 0;  // its fault snapshots: hcrc_ctx::h_faults[2 index ..] (1 .. kMaxLanes)
 };
 
 // Host ranges pinned (hcrc_host_alloc) or registered (hcrc_host_register)
@@ -258,6 +262,13 @@ struct hcrc_ctx {
   // stream-ordered scratch (size-class lists) from a private pool that keeps
   // its memory mapped between calls (release threshold: never)
   hipMemPool_t scratch_pool = nullptr;
+  // faults of the lane-packed kernels (crc32c_lds.h kFault*): the device's
+  // count of faulting waves (a module global, only ever grows), pinned
+  // snapshots of it (lane k: [2k] before its launches, [2k + 1] after), and
+  // the count hcrc_ctx_check last saw (launches on callers' streams)
+  const unsigned int* d_faults = nullptr;
+  unsigned int* h_faults = nullptr;
+  std::atomic<unsigned int> faults_seen{0};
   // lanes of synchronous calls
   std::mutex lanes_mu;
   std::condition_variable lanes_cv;
@@ -281,6 +292,7 @@ class LaneLease {
       if (static_cast<int>(ctx->lanes.size()) < kMaxLanes) {
         ctx->lanes.emplace_back(new Lane);
         lane_ = ctx->lanes.back().get();
+        lane_->index = static_cast<int>(ctx->lanes.size());
         return;
       }
       ctx->lanes_cv.wait(lk);
@@ -312,6 +324,21 @@ class LaneLease {
   int Stream() {
     if (!lane_->stream) HCRC_CHECK(hipStreamCreateWithFlags(&lane_->stream, hipStreamNonBlocking));
     return HCRC_OK;
+  }
+  // The device's fault count before the call's launches (stream order).
+  int FaultsBefore() {
+    HCRC_CHECK(hipMemcpyAsync(ctx_->h_faults + 2 * lane_->index, ctx_->d_faults, 4,
+                              hipMemcpyDeviceToHost, lane_->stream));
+    return HCRC_OK;
+  }
+  // After the call's launches: HCRC_ERR_KERNEL if the count grew (one of
+  // them -- or, conservatively, a concurrent call's -- left a span
+  // uncomputed), else HCRC_OK.  Waits for the stream.
+  int CheckFaults() {
+    unsigned int* h = ctx_->h_faults + 2 * lane_->index;
+    HCRC_CHECK(hipMemcpyAsync(h + 1, ctx_->d_faults, 4, hipMemcpyDeviceToHost, lane_->stream));
+    HCRC_CHECK(hipStreamSynchronize(lane_->stream));
+    return h[1] != h[0] ? HCRC_ERR_KERNEL : HCRC_OK;
   }
   // Stream and staging slots.
   int Staging() {
@@ -467,6 +494,34 @@ int LaunchLong(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const ui
 // (the spans kernel shares long spans over a workgroup's waves).
 constexpr size_t kAutoLongSpans = 16;
 
+#ifdef WIPDB_HCRC_TEST_HOOKS
+// Test build only (make testlib, tests/test_gpu_parity.py): with
+// WIPDB_HCRC_FORCE_FAULT=1 every lane-packed launch reports a fault (its
+// error word set after it, as the kernel would) -- the HCRC_ERR_KERNEL paths.
+bool ForcedFault() {
+  static const bool on = [] {
+    const char* e = getenv("WIPDB_HCRC_FORCE_FAULT");
+    return e && *e == '1';
+  }();
+  return on;
+}
+#endif
+
+// A lane-packed launch is done: with the test build's forced fault, a fault
+// is counted after it, as a faulting launch would count it.
+int LaunchedLp(hipStream_t st) {
+  int rc = Launched();
+#ifdef WIPDB_HCRC_TEST_HOOKS
+  if (rc == HCRC_OK && ForcedFault()) {
+    hipLaunchKernelGGL(crc32c_lds_fault_probe_kernel, dim3(1), dim3(64), 0, st);
+    rc = Launched();
+  }
+#else
+  (void)st;
+#endif
+  return rc;
+}
+
 // Descriptor batch on device memory, enqueued on st.
 int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
                 const uint32_t* init, uint32_t* out, size_t count, int flags, hipStream_t st) {
@@ -492,7 +547,7 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                          lk::kLdsBytes, st, static_cast<const uint8_t*>(base), off + pos,
                          len + pos, init ? init + pos : nullptr, out + pos,
                          static_cast<uint64_t>(n), mask ? lk::kFlagMask : 0u, ctx->d_image);
-      rc = Launched();
+      rc = LaunchedLp(st);
     }
     if (rc) return rc;
   }
@@ -592,18 +647,24 @@ class CopyPool {
 };
 std::atomic<bool> CopyPool::g_forked_child{false};
 
-// Test hook (fault injection, tests/test_gpu_parity.py): with
-// WIPDB_HCRC_FAIL_PIECE=k in the environment, the first host batch that
-// reaches its k-th piece fails there with HCRC_ERR_LAUNCH while the previous
-// piece is still in flight -- the error path LaneLease must clean up.  Fires
-// once per process.
+// Test hook (fault injection; the test build only, make testlib,
+// tests/test_gpu_parity.py): with WIPDB_HCRC_FAIL_PIECE=k in the
+// environment, the first host batch that reaches its k-th piece fails there
+// with HCRC_ERR_LAUNCH while the previous piece is still in flight -- the
+// error path LaneLease must clean up.  Fires once per process.  The product
+// library has no hook: the environment cannot change what it does.
 bool InjectedPieceFault(size_t piece) {
+#ifdef WIPDB_HCRC_TEST_HOOKS
   static const long at = [] {
     const char* e = getenv("WIPDB_HCRC_FAIL_PIECE");
     return e && *e ? atol(e) : -1L;
   }();
   static std::atomic<bool> fired{false};
   return at >= 0 && piece == static_cast<size_t>(at) && !fired.exchange(true);
+#else
+  (void)piece;
+  return false;
+#endif
 }
 
 // Copy spans [lo, hi) into a slot's pinned buffer, keeping each span's
@@ -637,6 +698,7 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
                   const uint8_t* host_base, const uint64_t* offsets, const uint32_t* lengths,
                   const uint32_t* inits, uint32_t* out, size_t count, int flags) {
   const hipStream_t st = lane->stream;
+  if (const int frc = lane.FaultsBefore()) return frc;
   size_t i = 0, piece = 0;
   int k = 0;
   while (i < count) {
@@ -665,7 +727,7 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     const int rc = s.Drain();
     if (rc) return rc;
   }
-  return HCRC_OK;
+  return lane.CheckFaults();
 }
 
 int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
@@ -676,6 +738,7 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
   if (const uint8_t* dev = MappedSpans(base, offsets, lengths, count))
     return BatchZeroCopy(ctx, lane, dev, base, offsets, lengths, inits, out, count, flags);
   const hipStream_t st = lane->stream;
+  if (const int frc = lane.FaultsBefore()) return frc;
   size_t i = 0, piece = 0;
   int k = 0;
   while (i < count) {
@@ -714,7 +777,7 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     rc = s.Drain();
     if (rc) return rc;
   }
-  return HCRC_OK;
+  return lane.CheckFaults();
 }
 
 // Long spans of a host batch (SURVEY 5's long-context analogue): a span of
@@ -843,6 +906,7 @@ const char* hcrc_strerror(int code) {
     case HCRC_ERR_LAUNCH: return "kernel launch failed";
     case HCRC_ERR_MISMATCH: return "checksum mismatch";
     case HCRC_ERR_BOUNDS: return "span outside the base buffer";
+    case HCRC_ERR_KERNEL: return "a kernel reported an internal fault (outputs incomplete)";
     default: return "unknown error";
   }
 }
@@ -889,6 +953,11 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
   };
   for (const void* k : kernels)
     HCRC_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lk::kLdsBytes));
+  ctx->d_faults = lk::LpFaultCounter();
+  if (!ctx->d_faults) return HCRC_ERR_HIP;
+  HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_faults), 8 * (kMaxLanes + 1)));
+  HCRC_CHECK(hipMemcpy(ctx->h_faults, ctx->d_faults, 4, hipMemcpyDeviceToHost));
+  ctx->faults_seen = ctx->h_faults[0];
   {
     std::vector<uint32_t> img(lk::kImageBytes / 4);
     lk::BuildLdsImage(img.data());
@@ -916,6 +985,7 @@ int hcrc_ctx_destroy(hcrc_ctx* ctx) {
   }
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->d_image) (void)hipFree(ctx->d_image);
+  if (ctx->h_faults) (void)hipHostFree(ctx->h_faults);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->scratch_pool) {
     (void)hipDeviceSynchronize();
@@ -938,12 +1008,12 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const u
   if (flags & HCRC_DEVICE_PTRS) {
     LaneLease lane(ctx);
     int rc = lane.Stream();
+    if (rc == HCRC_OK) rc = lane.FaultsBefore();
     if (rc == HCRC_OK)
       rc = LaunchSpans(ctx, base, offsets, lengths, init_crcs, out_crcs, count, flags,
                        lane->stream);
     if (rc) return rc;
-    HCRC_CHECK(hipStreamSynchronize(lane->stream));
-    return HCRC_OK;
+    return lane.CheckFaults();
   }
   return BatchHostLong(ctx, static_cast<const uint8_t*>(base), offsets, lengths, init_crcs,
                        out_crcs, count, flags);
@@ -977,7 +1047,7 @@ int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
                        lk::kLdsBytes, st, static_cast<const uint8_t*>(d_base) + pos * stride,
                        stride, length, init_crc, d_out_crcs + pos, static_cast<uint64_t>(n),
                        static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_image);
-    const int rc = Launched();
+    const int rc = LaunchedLp(st);
     if (rc) return rc;
   }
   return HCRC_OK;
@@ -1004,7 +1074,7 @@ int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_of
       hipLaunchKernelGGL(lk::crc32c_lds_verify_kernel, dim3(LdsGrid(ctx, n)), dim3(lk::kThreads),
                          lk::kLdsBytes, st, static_cast<const uint8_t*>(d_base), d_offsets + pos,
                          d_lengths + pos, d_status + pos, static_cast<uint64_t>(n), ctx->d_image);
-      rc = Launched();
+      rc = LaunchedLp(st);
     }
     if (rc) return rc;
   }
@@ -1080,11 +1150,26 @@ int hcrc_fill_splitmix64_async(hcrc_ctx* ctx, void* d_dst, uint64_t nbytes, uint
   return Launched();
 }
 
-int hcrc_sync(hcrc_ctx* ctx, void* stream) {
+int hcrc_ctx_check(hcrc_ctx* ctx) {
   if (!ctx) return HCRC_ERR_INVALID;
   HCRC_DEVICE(ctx);
-  HCRC_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-  return HCRC_OK;
+  // the device's count, read after the launches already complete (the caller
+  // synchronised the streams it launched on); slot 0 of the snapshots is the
+  // context's own (lanes use 2 .. 2 kMaxLanes + 1)
+  std::lock_guard<std::mutex> lk(ctx->lanes_mu);
+  HCRC_CHECK(hipMemcpyAsync(ctx->h_faults, ctx->d_faults, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HCRC_CHECK(hipStreamSynchronize(ctx->stream));
+  const unsigned int now = ctx->h_faults[0];
+  return ctx->faults_seen.exchange(now) != now ? HCRC_ERR_KERNEL : HCRC_OK;
+}
+
+int hcrc_sync(hcrc_ctx* ctx, void* stream) {
+  if (!ctx) return HCRC_ERR_INVALID;
+  {
+    HCRC_DEVICE(ctx);
+    HCRC_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  }
+  return hcrc_ctx_check(ctx);
 }
 
 int hcrc_batch_multi_ex(const int* devices, int ndev, const void* base, const uint64_t* offsets,
