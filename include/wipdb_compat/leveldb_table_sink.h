@@ -30,9 +30,10 @@
 // leveldb-side byte identity is parity-unpinned beyond that kv equivalence.
 //
 // Only inline members of leveldb's headers are used, so including this file
-// links against no leveldb library.  Compression must be kNoCompression
-// (WipDB's benchmarks run without it, kv_bench.cc:984); SupportedOptions
-// says whether a leveldb::Options can be served.
+// links against no leveldb library.  SupportedOptions says whether a
+// leveldb::Options can be served (no compression -- WipDB's benchmarks run
+// without it, kv_bench.cc:984 -- a bytewise or internal-over-bytewise
+// comparator, no filter or the built-in bloom filter); call it first.
 #pragma once
 #include <string.h>
 
@@ -40,6 +41,7 @@
 
 #include "leveldb/comparator.h"
 #include "leveldb/env.h"
+#include "leveldb/filter_policy.h"
 #include "leveldb/options.h"
 #include "leveldb/slice.h"
 #include "leveldb/status.h"
@@ -69,13 +71,35 @@ class WritableFileSink : public table::TableSink {
 };
 
 // Whether wipdb::table can write what leveldb::TableBuilder would for these
-// options: no compression (the builder stores blocks raw).
+// options.  Anything else must stay on leveldb::TableBuilder, since
+// TableOptionsFrom would write a different (valid-looking) table:
+//   * no compression (the builder stores blocks raw);
+//   * comparator "leveldb.BytewiseComparator" (leveldb's default), or
+//     "leveldb.InternalKeyComparator" (leveldb/db/dbformat.cc:46-48) over a
+//     bytewise user comparator -- the wrapped comparator is not visible
+//     through leveldb's public headers, so the caller confirms it
+//     (internal_user_bytewise); index separators and successors are computed
+//     bytewise on the (user) key, any other order would misplace lookups;
+//   * no filter policy, or one named "leveldb.BuiltinBloomFilter2"
+//     (leveldb/util/bloom.cc; the InternalFilterPolicy wrapping it reports the
+//     same name, dbformat.cc:101-103): the meta entry "filter.<Name>" and the
+//     filter bytes are the built-in bloom filter's.
 template <class Opts = leveldb::Options>
-inline bool SupportedOptions(const Opts& o) {
-  return o.compression == leveldb::kNoCompression;
+inline bool SupportedOptions(const Opts& o, bool internal_user_bytewise = false) {
+  if (o.compression != leveldb::kNoCompression) return false;
+  const char* cmp = o.comparator ? o.comparator->Name() : "leveldb.BytewiseComparator";
+  if (strcmp(cmp, "leveldb.InternalKeyComparator") == 0) {
+    if (!internal_user_bytewise) return false;
+  } else if (strcmp(cmp, "leveldb.BytewiseComparator") != 0) {
+    return false;
+  }
+  if (o.filter_policy && strcmp(o.filter_policy->Name(), "leveldb.BuiltinBloomFilter2") != 0)
+    return false;
+  return true;
 }
 
-// The table options a leveldb::Options stands for.  leveldb::FilterPolicy
+// The table options a leveldb::Options stands for (only for options
+// SupportedOptions accepts).  leveldb::FilterPolicy
 // does not expose its bits per key, so the caller passes what it gave
 // NewBloomFilterPolicy (0 = no filter policy).  A comparator named
 // "leveldb.InternalKeyComparator" (leveldb/db/dbformat.cc) selects internal

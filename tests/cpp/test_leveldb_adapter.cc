@@ -32,7 +32,7 @@ __attribute__((used)) void Instantiate(leveldb::WritableFile* f, const leveldb::
   wipdb::leveldbcompat::WritableFileSink<> sink(f);
   wipdb::table::TableBuilder tb(
       wipdb::leveldbcompat::TableOptionsFrom(*o, 10, wipdb::table::CrcMode::kBatchAuto), &sink);
-  (void)wipdb::leveldbcompat::SupportedOptions(*o);
+  (void)wipdb::leveldbcompat::SupportedOptions(*o, true);
   (void)wipdb::leveldbcompat::ReadImage(r, 100, img);
 }
 
@@ -63,11 +63,15 @@ struct NamedComparator {
   const char* name;
   const char* Name() const { return name; }
 };
+struct NamedPolicy {
+  const char* name;
+  const char* Name() const { return name; }
+};
 // leveldb::Options's fields the adapter reads
 struct Opts {
   size_t block_size;
   int block_restart_interval;
-  const void* filter_policy;
+  const NamedPolicy* filter_policy;
   const NamedComparator* comparator;
   leveldb::CompressionType compression;
 };
@@ -97,14 +101,32 @@ int main(int argc, char** argv) {
   const uint32_t n = u32();
   const int bloom = atoi(argv[5]);
   const NamedComparator icmp{"leveldb.InternalKeyComparator"}, bcmp{"leveldb.BytewiseComparator"};
-  static const int kPolicy = 0;
-  Opts o{static_cast<size_t>(atol(argv[3])), atoi(argv[4]), bloom ? &kPolicy : nullptr,
-         atoi(argv[6]) ? &icmp : &bcmp, leveldb::kNoCompression};
+  static const NamedPolicy kBloom{"leveldb.BuiltinBloomFilter2"};
+  const bool internal = atoi(argv[6]) != 0;
+  Opts o{static_cast<size_t>(atol(argv[3])), atoi(argv[4]), bloom ? &kBloom : nullptr,
+         internal ? &icmp : &bcmp, leveldb::kNoCompression};
   const auto mode = static_cast<wipdb::table::CrcMode>(atoi(argv[7]));
-  if (!wipdb::leveldbcompat::SupportedOptions(o)) return 3;
-  Opts snappy = o;
-  snappy.compression = leveldb::kSnappyCompression;
-  if (wipdb::leveldbcompat::SupportedOptions(snappy)) return 3;
+  if (!wipdb::leveldbcompat::SupportedOptions(o, true)) return 3;
+  // options the adapter must refuse: compression, a custom
+  // comparator, an internal comparator whose user comparator is not
+  // confirmed bytewise, a filter policy other than the built-in bloom filter
+  Opts bad = o;
+  bad.compression = leveldb::kSnappyCompression;
+  if (wipdb::leveldbcompat::SupportedOptions(bad, true)) return 3;
+  static const NamedComparator rev{"leveldb.ReverseBytewiseComparator"};
+  bad = o;
+  bad.comparator = &rev;
+  if (wipdb::leveldbcompat::SupportedOptions(bad, true)) return 3;
+  bad = o;
+  bad.comparator = &icmp;
+  if (wipdb::leveldbcompat::SupportedOptions(bad, false)) return 3;
+  static const NamedPolicy custom{"my.PrefixFilter"};
+  bad = o;
+  bad.filter_policy = &custom;
+  if (wipdb::leveldbcompat::SupportedOptions(bad, true)) return 3;
+  bad = o;
+  bad.comparator = nullptr;  // leveldb's default: bytewise
+  if (!internal && !wipdb::leveldbcompat::SupportedOptions(bad, false)) return 3;
 
   MemFile file;
   wipdb::leveldbcompat::WritableFileSink<MemFile> sink(&file);

@@ -23,8 +23,8 @@ REF_SO = os.path.join(REPO, "oracle", "_ref", "libref_table.so")
 
 
 class RefLog:
-    def __init__(self):
-        lib = ctypes.CDLL(REF_SO)
+    def __init__(self, path: str = REF_SO):
+        lib = ctypes.CDLL(path)
         vp, sz = ctypes.c_void_p, ctypes.c_size_t
         lib.ref_log_write.restype = ctypes.c_long
         lib.ref_log_write.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_uint64, vp, sz]
@@ -95,11 +95,18 @@ class RefLog:
         return tw, tr
 
 
-@pytest.fixture(scope="module")
-def ref_log():
-    if not os.path.exists(REF_SO):
-        pytest.skip("oracle/_ref/libref_table.so not built (reference absent, no prebuilt copy)")
-    return RefLog()
+# "dropin": the reference's log_writer.cc / log_reader.cc with util/crc32c.cc
+# left out, their kv::crc32c::Extend / Value calls resolved from
+# libhip_crc32c_batch.so (oracle/Makefile DROPIN_SO)
+REF_DROPIN_SO = os.path.join(REPO, "oracle", "_ref", "libref_table_dropin.so")
+
+
+@pytest.fixture(scope="module", params=["reference", "dropin"])
+def ref_log(request):
+    path = REF_SO if request.param == "reference" else REF_DROPIN_SO
+    if not os.path.exists(path):
+        pytest.skip(f"{os.path.relpath(path, REPO)} not built (reference absent, no prebuilt copy)")
+    return RefLog(path)
 
 
 def records(n: int, seed: int):
