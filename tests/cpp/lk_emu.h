@@ -269,7 +269,6 @@ inline void dma1nt(uint64_t base, uint32_t dst, uint32_t off) {
   emu::copy16(dst + 16u * emu::lane(), base + off);
 }
 inline void dma1v(uint64_t addr, uint32_t dst) { emu::copy16(dst + 16u * emu::lane(), addr); }
-inline void dma1v_c(uint64_t addr, uint32_t dst) { emu::copy16(dst + 16u * emu::lane(), addr); }
 // the wave's DMAs have landed: the lanes meet (each copied its chunks at issue)
 template <int N>
 inline void wait_vm() {

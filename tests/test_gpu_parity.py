@@ -289,13 +289,14 @@ def test_host_batch_long_spans_split(engine, oracle):
     np.testing.assert_array_equal(engine.batch(buf, offs, lens), oracle.batch(buf, offs, lens))
 
 
-def test_device_batch_split_long(engine, oracle):
+def test_device_batch_split_long(engine, oracle, reference):
     """HCRC_SPLIT_LONG: device spans of >= 128 KiB in 16 KiB parts on many
     waves, combined by linearity (crc32c_util.hip split_* kernels): lengths
     around the cut and the part edges, odd offsets, inits, masked output,
     short spans in between, a lone 5 MiB span, a lone span past the smallest
-    part pool (1 GiB + ...: stays whole); and the flag combined with
-    HCRC_SPLIT_SMALL -- against the oracle."""
+    part pool (1 GiB + ...: stays whole, checked against the compiled
+    reference); and the flag combined with HCRC_SPLIT_SMALL -- against the
+    oracle."""
     rng = np.random.default_rng(65536)
     buf = rng.integers(0, 256, 12 << 20, dtype=np.uint8)
     K = 1 << 10
@@ -329,14 +330,14 @@ def test_device_batch_split_long(engine, oracle):
     out = engine.batch_device(big, _t(bo), _t(bl), split_long=True)
     host_tail = big[-(1 << 20):].cpu().numpy()
     want_small = oracle.batch(host_tail, bo[1:] - np.uint64(nbig - host_tail.size), bl[1:])
-    # the spans kernel's answer (17 spans: past the automatic split of tiny
-    # device batches; the 16 empty ones just return their init)
-    pad_o = np.concatenate([bo[:1], np.zeros(16, np.uint64)])
-    pad_l = np.concatenate([bl[:1], np.zeros(16, np.uint32)])
-    ref_big = engine.batch_device(big, _t(pad_o), _t(pad_l))
+    # the 1 GiB span against the compiled reference on a host copy of its
+    # bytes (not the spans kernel's own answer)
+    host_big = big[1:1 + int(bl[0])].cpu().numpy()
+    want_big = reference.extend(0, host_big)
+    del host_big
     got = _u32(out)
     assert int(got[1]) == int(want_small[0])
-    assert int(got[0]) == int(_u32(ref_big)[0])
+    assert int(got[0]) == want_big
     del big
     torch.cuda.synchronize()
 

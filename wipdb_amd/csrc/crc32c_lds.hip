@@ -38,16 +38,6 @@
 
 #include "crc32c_dev.h"
 
-// The batch DMA: 1 = every lane loads its own stripe's 4 chunks (per-lane
-// addresses, no exchange); 0 = the segment DMA's layout (lane m of
-// instruction q loads chunk m % 4 of stripe 16 q + m / 4, addresses
-// exchanged by ds_bpermute) -- an A/B build.
-// (own stripes measured slower on every short bucket: the uncoalesced DMA
-// instructions cost more than the exchange, profiles/r03g_ab.log)
-#ifndef WIPDB_LP_OWN_STRIPE_DMA
-#define WIPDB_LP_OWN_STRIPE_DMA 0
-#endif
-
 namespace wipdb {
 namespace lk {
 
@@ -76,37 +66,15 @@ constexpr uint32_t kEagerSegs = WIPDB_LP_EAGER_SEGS;
 #define WIPDB_LP_PRIO 3
 #endif
 constexpr int kPrio = WIPDB_LP_PRIO;
-// Batch DMA addresses: the high words exchanged only when they differ
-// between stripes (1) or always (0)
-#ifndef WIPDB_LP_HI_UNI
-#define WIPDB_LP_HI_UNI 0
-#endif
-// The batch path's per-lane selects (the DMA's chunk sources, the tail word,
-// the head chunk's fix) as explicit v_cndmask on ballot masks (1) or as ?:
-// chains (0: hipcc lowered some into exec-masked branches; 1: config 3's
-// 512 B / 1 KiB / 2 KiB buckets +7 %, same session, profiles/r03v2_vsel_ab.log)
-#ifndef WIPDB_LP_VSEL
-#define WIPDB_LP_VSEL 1
-#endif
-// MakeStripe's per-lane select on a ballot mask too (1; no measurable
-// change, profiles/r03v3_stripe_atomicopt_ab.log: one exec-masked branch fewer)
-#ifndef WIPDB_LP_VSEL2
-#define WIPDB_LP_VSEL2 1
-#endif
-// The batch DMA nontemporal (1) or through the caches (0, an A/B build)
-#ifndef WIPDB_LP_BATCH_NT
-#define WIPDB_LP_BATCH_NT 1
-#endif
-
-// Wave scans: rows joined by DPP row broadcasts (1: short buckets and the mix
-// +0.5-1 %, same session, profiles/r03v4_bcast_ab.log) or through readlane (0)
-#ifndef WIPDB_LP_BCAST
-#define WIPDB_LP_BCAST 1
-#endif
-// the wave OR too (1, A/B)
-#ifndef WIPDB_LP_BCAST_OR
-#define WIPDB_LP_BCAST_OR 0
-#endif
+// (Variants measured and dropped, same-session A/B under profiles/: each lane
+// DMA-ing its own stripe instead of the exchanged segment layout, -3..-12 %
+// on short buckets, r03g_ab.log; the batch DMA through the caches, within
+// noise, r03z_bnt_hiu_ab.log; exchanging the stripes' high address words only
+// when they differ, within noise, same log; the per-lane selects as ?:
+// chains, which hipcc lowered into exec-masked branches, short buckets -7 %,
+// r03v2_vsel_ab.log; wave scans joined through readlane instead of DPP row
+// broadcasts, -0.5..1 %, r03v4_bcast_ab.log; the wave OR by row broadcasts,
+// mixed, r03v5_bcast_or_ab.log.)
 
 // Bound of the long-span queue's spins (a popper waiting for its record's
 // producer, a producer waiting for a slot to be freed): never reached while
@@ -118,43 +86,29 @@ constexpr int kPrio = WIPDB_LP_PRIO;
 #endif
 
 // ---------------------------------------------------------------------------
-// Wave scans (row-local DPP steps, rows joined through readlane)
+// Wave scans (row-local DPP steps, rows joined by DPP row broadcasts)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t scan_add(uint32_t v, uint32_t l) {
+__device__ __forceinline__ uint32_t scan_add(uint32_t v) {
   v += dpp<0x111>(v);  // row_shr:1 (lanes without a source read 0)
   v += dpp<0x112>(v);  // row_shr:2
   v += dpp<0x114>(v);  // row_shr:4
   v += dpp<0x118>(v);  // row_shr:8
-#if WIPDB_LP_BCAST
-  v += bcast15(v);     // rows joined by DPP row broadcasts
-  return v + bcast31(v);
-#endif
-  const uint32_t r0 = rdlane(v, 15), r1 = rdlane(v, 31),
-                 r2 = rdlane(v, 47);
-  return v + (l >= 16u ? r0 : 0u) + (l >= 32u ? r1 : 0u) + (l >= 48u ? r2 : 0u);
+  v += bcast15(v);     // rows 1, 3 += lane 15 of the row before
+  return v + bcast31(v);  // rows 2, 3 += lane 31
 }
-__device__ __forceinline__ uint32_t scan_xor(uint32_t v, uint32_t l) {
+__device__ __forceinline__ uint32_t scan_xor(uint32_t v) {
   v ^= dpp<0x111>(v);
   v ^= dpp<0x112>(v);
   v ^= dpp<0x114>(v);
   v ^= dpp<0x118>(v);
-#if WIPDB_LP_BCAST
   v ^= bcast15(v);
   return v ^ bcast31(v);
-#endif
-  const uint32_t r0 = rdlane(v, 15), r1 = rdlane(v, 31),
-                 r2 = rdlane(v, 47);
-  return v ^ (l >= 16u ? r0 : 0u) ^ (l >= 32u ? r1 : 0u) ^ (l >= 48u ? r2 : 0u);
 }
 __device__ __forceinline__ uint32_t scan_or(uint32_t v) {  // the OR of the wave (uniform)
   v |= dpp<0x111>(v);
   v |= dpp<0x112>(v);
   v |= dpp<0x114>(v);
   v |= dpp<0x118>(v);
-#if WIPDB_LP_BCAST_OR
-  v |= bcast15(v);
-  return rdlane(v | bcast31(v), 63);
-#endif
   return rdlane(v, 15) | rdlane(v, 31) |
          rdlane(v, 47) | rdlane(v, 63);
 }
@@ -203,16 +157,9 @@ __device__ __forceinline__ uint32_t residue_of(uint32_t jv) {
 }
 
 // Word e / 4 .. of the 16 bytes c0..c3 at byte e (per lane; e + 4 may pass
-// byte 16 -- only the low k <= 3 bytes of a tail word are used).
-__device__ __forceinline__ uint32_t word_at(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                            uint32_t e) {
-  const uint32_t q = e >> 2, sh = 8u * (e & 3u);
-  const uint32_t lo = q == 0u ? c0 : (q == 1u ? c1 : (q == 2u ? c2 : c3));
-  const uint32_t hi = q == 0u ? c1 : (q == 1u ? c2 : (q == 2u ? c3 : 0u));
-  return sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
-}
-
-// word_at with the selects on ballot masks (all lanes call it)
+// byte 16 -- only the low k <= 3 bytes of a tail word are used), with the
+// selects on ballot masks (all lanes call it; hipcc turned ?: chains into
+// exec-masked branches)
 __device__ __forceinline__ uint32_t word_at_v(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t e) {
   const uint32_t q = e >> 2;
@@ -315,10 +262,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     k1b |= (128u + 4u * t) << (8 * j);
     k2b |= (8u * t) << (8 * j);
   }
-#if !WIPDB_LP_OWN_STRIPE_DMA
   const uint32_t dsl = l >> 2;                          // stripe lane 16 q + dsl
   const uint32_t dci = ((l & 3u) - (l >> 4)) & 3u;      // chunk of that stripe
-#endif
 
   // ---- the piece ring: entry q in lane q ----
   uint32_t rp_lo = 0, rp_hi = 0, rpw = 0, rinj = 0, rid = 0;
@@ -587,7 +532,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t rank = mbcnt_lo(dshort, 0u);
     const bool tk = l < kDesk && ((dshort >> (l & (kDesk - 1u))) & 1u) != 0u && rank < take;
     const uint32_t tmask = static_cast<uint32_t>(ballot(tk));
-    const uint32_t nl_sum = scan_add(tk ? PW{dpw}.nl() : 0u, l);
+    const uint32_t nl_sum = scan_add(tk ? PW{dpw}.nl() : 0u);
     // ring lane q in [rcnt, rcnt + take) pulls the (q - rcnt)-th short lane
     const uint32_t kq = l - rcnt;
     uint32_t pos = 0;
@@ -642,7 +587,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   auto issue_batch = [&]() {
     const PW rw{rpw};
     const uint32_t rem = l < rcnt ? rw.rem() : 0u;
-    const uint32_t incl = scan_add(rem, l);
+    const uint32_t incl = scan_add(rem);
     const bool tk = l < rcnt && incl <= 64u;
     const uint32_t n = static_cast<uint32_t>(__builtin_popcountll(ballot(tk)));  // >= 1
     const uint32_t usedf = rdlane(incl, n - 1u);
@@ -662,58 +607,23 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
     const uint32_t b_st = bperm(st, e);
     const PW pw{live ? b_pw : 0u};
     const uint32_t j = live ? pw.j0() + (l - b_st) : 0u;  // the lane's stripe of its piece
-#if WIPDB_LP_VSEL2
     const Stripe sp = make_stripe_v(pw, j);
-#else
-    const Stripe sp = MakeStripe(pw, j);
-#endif
     const uint64_t S = sbase + ((static_cast<uint64_t>(b_hi) << 32) | b_lo) +
                        static_cast<uint64_t>(sp.s);
     const uint32_t s_lo = static_cast<uint32_t>(S), s_hi = static_cast<uint32_t>(S >> 32);
-#if WIPDB_LP_OWN_STRIPE_DMA
-    // instruction q: lane l DMAs chunk q of its own stripe into slot byte
-    // 1024 q + 16 l (no address exchange; the loop top reads the batch's
-    // stripes back lane-linear, conflict-free)
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-      const uint64_t a = S + static_cast<uint64_t>(StripeChunkSrc(sp.info, q));
-      if (live) dma1v(a, pp.slot + 1024u * q);
-    }
-#else
-#if WIPDB_LP_HI_UNI
-    // the stripes' high address words are one value when the batch's pieces
-    // lie in one 4 GiB window (lane 0 is always live): then only the low
-    // words and the stripe info travel
-    const uint32_t h0 = rdlane(s_hi, 0);
-    const bool hu = ballot(live && s_hi != h0) == 0u;
-#endif
+    // instruction q: lane m loads chunk dci of stripe 16 q + dsl (the
+    // segment DMA's layout), its address from the lane that owns the stripe
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
       const uint32_t sl = 16u * q + dsl;
-#if WIPDB_LP_HI_UNI
-      const uint32_t x_lo = bperm(s_lo, sl), x_in = bperm(sp.info, sl);
-      uint32_t x_hi = h0;
-      if (!hu) x_hi = bperm(s_hi, sl);
-#else
       const uint32_t x_lo = bperm(s_lo, sl), x_hi = bperm(s_hi, sl), x_in = bperm(sp.info, sl);
-#endif
-#if WIPDB_LP_VSEL
       // StripeChunkSrc(x_in, dci) on ballot masks
       const uint32_t fr = x_in & 7u;
       const uint64_t lt = ballot(dci < fr), eq = ballot(dci == fr && (x_in & 8u) != 0u);
       const uint32_t off = vsel(lt, x_in >> 6, 16u * dci + vsel(eq, (x_in >> 2) & 12u, 0u));
       const uint64_t a = ((static_cast<uint64_t>(x_hi) << 32) | x_lo) + off;
-#else
-      const uint64_t a = ((static_cast<uint64_t>(x_hi) << 32) | x_lo) +
-                         static_cast<uint64_t>(StripeChunkSrc(x_in, dci));
-#endif
-#if WIPDB_LP_BATCH_NT
       if (sl < used) dma1v(a, pp.slot + 1024u * q);
-#else
-      if (sl < used) dma1v_c(a, pp.slot + 1024u * q);
-#endif
     }
-#endif
     nb_pw = pw.v;
     nb_inj = b_inj;
     nb_id = b_id;
@@ -934,22 +844,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       cb_id = nb_id;
       cb_j = nb_j;
       const uint32_t idle_w = lds_ld_sync(MiscAddr(kMiscIdle));  // (rides with the slot's reads)
-#if WIPDB_LP_OWN_STRIPE_DMA
-      if ((ck & 3u) == kWBatch) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const u32x4 d = lds_ld4(pp.slot + 16u * l + 1024u * q);
-          W[4 * q] = d.x;
-          W[4 * q + 1] = d.y;
-          W[4 * q + 2] = d.z;
-          W[4 * q + 3] = d.w;
-        }
-      } else {
-        pp.read(W);
-      }
-#else
       pp.read(W);
-#endif
       if ((ck & 3u) == kWSeg && (cs.fl & kSAux)) ax = lds_ld4(SegAuxAddr(w));
       pp.release();
       idle = uni(idle_w);
@@ -979,11 +874,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       const uint32_t j = cb_j, nl = pw.nl(), r = pw.r();
       const int32_t f = static_cast<int32_t>(pw.front()) - 4 * static_cast<int32_t>(j);
       // lane 0 of a piece with a tail: its chunk 0 is the aux chunk
-#if WIPDB_LP_VSEL
       const uint32_t tw = word_at_v(W[0], W[1], W[2], W[3], pw.te());
-#else
-      const uint32_t tw = word_at(W[0], W[1], W[2], W[3], pw.te());
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bool z = !live || i < f;
@@ -994,7 +885,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       if (ballot(live && r != 0u && f >= 0 && f < 4) != 0u) {
         const bool has = live && r != 0u && f >= 0 && f < 4;
         uint32_t c[4];
-#if WIPDB_LP_VSEL
         const uint64_t f1 = ballot(f == 1), f2 = ballot(f == 2), f3 = ballot(f == 3);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -1006,16 +896,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
 #pragma unroll
           for (int q = 0; q < 4; ++q) W[4 * i + q] = vsel(hi, c[q], W[4 * i + q]);
         }
-#else
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          c[q] = f == 0 ? W[q] : (f == 1 ? W[4 + q] : (f == 2 ? W[8 + q] : W[12 + q]));
-        fix_head(c, pw.hp(), pw.ws(), cb_inj);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) W[4 * i + q] = has && f == i ? c[q] : W[4 * i + q];
-#endif
       }
       if (kV) {
         uint32_t lo = W[14], hi = W[15];
@@ -1027,7 +907,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       const uint32_t R = scan(lk, W);
       const uint32_t d = live ? nl - 1u - j : 0u;  // lanes of the piece after this one
       const uint32_t v = shift64(lk, k1b, k2b, R, d);
-      const uint32_t xs = scan_xor(v, l);
+      const uint32_t xs = scan_xor(v);
       // the piece's lanes in this batch end at lane l + min(d, 63 - l): the
       // XOR over them, at its first lane here (j == j0)
       const uint32_t last = l + (d < 63u - l ? d : 63u - l);

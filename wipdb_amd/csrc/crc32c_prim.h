@@ -221,21 +221,6 @@ __device__ __forceinline__ void dma1v(uint64_t addr, uint32_t dst) {
       : "memory");
 }
 
-// The same through the caches (no nt): lines at span edges, shared with the
-// neighbouring span, may then hit in L2 -- an A/B build of the batch DMA.
-__device__ __forceinline__ void dma1v_c(uint64_t addr, uint32_t dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(addr), "s"(dst)
-      : "memory");
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
