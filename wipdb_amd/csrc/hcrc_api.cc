@@ -564,6 +564,13 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
 constexpr size_t kAutoSplitMin = 256;
 constexpr uint32_t kAutoSplitChunks = 80;
 int AutoSplit(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, size_t n) {
+#ifdef WIPDB_HCRC_TEST_HOOKS
+  // A/B of the choice itself (scripts/autosplit_ab.py): "0" never, "1" always
+  if (const char* e = getenv("WIPDB_HCRC_AUTOSPLIT")) {
+    if (*e == '0') return 0;
+    if (*e == '1') return HCRC_SPLIT_SMALL;
+  }
+#endif
   size_t hits = 0;
   for (size_t i = 0; i < n && hits < kAutoSplitMin; ++i) {
     const uint32_t h = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(base) + offsets[i]) & 15u);
