@@ -19,13 +19,21 @@ import torch  # noqa: E402
 
 from wipdb_amd import Engine  # noqa: E402
 
-NAMES = ["wait", "decide", "compute", "tail", "segs", "batches", "idle", "life"]
+NAMES = ["wait", "decide", "compute", "tail", "segs", "batches", "idle", "life",
+         "s_checks", "s_wait", "s_read_desk", "s_issue", "s_compute", "s_iters"]
+NPROF = 16
 
 
 def shape(name):
     if name == "headline":
         n = 1 << 20
         return np.arange(n, dtype=np.int64) * 4096, np.full(n, 4096, np.int32), n * 4096
+    if name == "tblocks":  # WriteRawBlock spans: 4097..4225 B (contents + type), SST-packed
+        rng = np.random.default_rng(5)
+        n = 1 << 20
+        ln = rng.integers(4097, 4226, n).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(ln + 4)[:-1]])
+        return offs.astype(np.int64), ln.astype(np.int32), int(offs[-1] + ln[-1] + 64)
     if name.startswith("bucket"):  # bucketN: SST-packed N-byte spans + 5-byte trailers
         b = int(name[6:])
         n = (4 << 30) // (b + 5)
@@ -34,11 +42,11 @@ def shape(name):
 
 
 def main():
-    shapes = sys.argv[1:] or ["headline", "bucket512", "bucket4096", "bucket65536"]
+    shapes = sys.argv[1:] or ["headline", "tblocks", "bucket512", "bucket4096", "bucket65536"]
     lib = ctypes.CDLL(PROF_LIB)
     fn = lib.hcrc_debug_lp_prof
     fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
-    host = np.zeros(4096 * 8, np.uint64)
+    host = np.zeros(4096 * NPROF, np.uint64)
     with Engine(0) as eng:
         for name in shapes:
             offs, lens, size = shape(name)
@@ -59,7 +67,7 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / reps
             assert fn(host.ctypes.data, host.nbytes, 1) == 0
-            p = host.reshape(4096, 8).astype(np.float64) / reps
+            p = host.reshape(4096, NPROF).astype(np.float64) / reps
             live = p[:, 7] > 0
             p = p[live]
             it = p[:, 4] + p[:, 5] + p[:, 6]
@@ -73,6 +81,12 @@ def main():
             per = p[:, :4].sum(axis=0) / max(it.sum(), 1)
             print("  cycles per iteration: " + ", ".join(
                 f"{NAMES[k]} {per[k]:.0f}" for k in range(4)) + f" (sum {per.sum():.0f})", flush=True)
+            si = p[:, 13].sum()
+            if si:
+                sp = p[:, 8:13].sum(axis=0) / si
+                print(f"  segment loop: {si / live.sum():.1f} iterations per wave; cycles per "
+                      "iteration: " + ", ".join(f"{NAMES[8 + k][2:]} {sp[k]:.0f}" for k in range(5))
+                      + f" (sum {sp.sum():.0f})", flush=True)
             del buf, o, ln, out
             torch.cuda.empty_cache()
 

@@ -31,6 +31,8 @@ for s in $STEPS; do
     mixed) run mixed 300 python scripts/bench_extra.py --what mixed ;;
     host) run host 400 python scripts/bench_extra.py --what sst,sstpin,host4k ;;
     long) run long 300 python scripts/long_span_probe.py ;;
+    lpprof) run lpprof 300 python -u scripts/debug/lp_prof.py ${LPPROF_SHAPES:-headline tblocks bucket512 bucket1024 bucket2048 bucket65536} ;;
+    autosplit) run autosplit 500 python -u scripts/autosplit_ab.py ;;
     cfg4) run cfg4 400 python bench.py --blocks 8388608 --steps 10 --warmup 5 ;;
     ab) run ab 900 bash scripts/gpu_abn.sh ${AB_ROUNDS:-2} ${AB_WHAT:-mixed,tblocks,vtblocks,verify} tree ${AB_LIBS:-build/ab/lib_r02.so} ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;

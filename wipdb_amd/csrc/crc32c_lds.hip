@@ -228,7 +228,8 @@ __device__ __forceinline__ void report_fault(uint32_t) {
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
 // Profiling build only: per wave, the cycles of each part of run_lp's loop
 // (s_memtime) and its iteration counts, summed over launches.
-__device__ unsigned long long g_lp_prof[4096 * 8];
+constexpr int kProfN = 16;  // accumulators per wave (scripts/debug/lp_prof.py NAMES)
+__device__ unsigned long long g_lp_prof[4096 * kProfN];
 #define LP_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
 #define LP_ACC(k, v) (prof[k] += (v))
 #else
@@ -766,7 +767,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // code stays small.
   bool have = false, stored_prev = false;
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
-  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prof[kProfN] = {};
   LP_T(t_start);
 #endif
   for (;;) {
@@ -781,6 +782,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       bool fidle = false;
 #pragma nounroll
       for (;;) {
+        LP_T(s0);
         // the desk is out of spans with segments: a span queued for the
         // workgroup, else the next desk if it is in, sorted, and holds only
         // spans with segments
@@ -790,8 +792,10 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
           switch_desk();
         if (!lvalid && (dlong == 0u || fidle)) break;
         if (rcnt >= 62u || rlanes + ((ns.fl & kSPush) ? PW{ns.pw}.nl() : 0u) >= 64u) break;  // a batch is due
+        LP_T(s1);
         if (stored_prev) wait_vm<1>();
         else wait_vm<0>();
+        LP_T(s2);
         if constexpr (kPrio != 0) lk_prio<kPrio>();
         if (nstate == 1u) {
           // the desk loads are older than the DMA just waited for: the
@@ -817,10 +821,19 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         // after it may stay in flight)
         if (nstate == 0u && !exhausted) grab_desk();
         if (!lvalid) take_own();
+        LP_T(s3);
         issue_seg();
         if constexpr (kPrio != 0) lk_prio<0>();
+        LP_T(s4);
         stored_prev = seg_compute(c, W, fax);
         fidle = uni(idle_w) != 0u;
+        LP_T(s5);
+        LP_ACC(8, s1 - s0);   // checks (pop, switch_desk, exits)
+        LP_ACC(9, s2 - s1);   // wait for the slot
+        LP_ACC(10, s3 - s2);  // read, sort / grab / take
+        LP_ACC(11, s4 - s3);  // issue the next DMA
+        LP_ACC(12, s5 - s4);  // compute
+        LP_ACC(13, 1u);
       }
     }
     LP_T(t0);
@@ -971,7 +984,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   prof[7] = t_end - t_start;
   if (l == 0u) {
     const uint32_t slot = (group_id() * static_cast<uint32_t>(kWaves) + w) & 4095u;
-    for (int k = 0; k < 8; ++k) atomicAdd(&g_lp_prof[slot * 8u + k], static_cast<unsigned long long>(prof[k]));
+    for (int k = 0; k < kProfN; ++k)
+      atomicAdd(&g_lp_prof[slot * kProfN + k], static_cast<unsigned long long>(prof[k]));
   }
 #endif
 }
@@ -1041,11 +1055,11 @@ unsigned int* LpFaultCounter() {
 // Profiling build only: copies (and with reset != 0 zeroes) g_lp_prof.
 extern "C" __attribute__((visibility("default"))) int hcrc_debug_lp_prof(void* host, uint64_t bytes,
                                                                           int reset) {
-  if (bytes > sizeof(unsigned long long) * 4096 * 8) return -1;
+  if (bytes > sizeof(unsigned long long) * 4096 * wipdb::lk::kProfN) return -1;
   if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(wipdb::lk::g_lp_prof), bytes) != hipSuccess)
     return -2;
   if (reset) {
-    static unsigned long long zero[4096 * 8];
+    static unsigned long long zero[4096 * wipdb::lk::kProfN];
     if (hipMemcpyToSymbol(HIP_SYMBOL(wipdb::lk::g_lp_prof), zero, sizeof(zero)) != hipSuccess)
       return -3;
   }
