@@ -115,9 +115,10 @@ const EnvConfig& Env() {
   return cfg;
 }
 
-// The process-wide context of a device (hcrc_ctx_shared, looked up per call:
-// a caller may have destroyed it), shared with hcrc_batch_multi; a device
-// that failed once is not retried.
+// The process-wide context of a device (hcrc_ctx_shared: created on first
+// use, it lives until the process ends -- hcrc_ctx_destroy refuses it), shared
+// with hcrc_batch_multi; a device whose context could not be created is not
+// retried.
 int CtxFor(int device, hcrc_ctx** out) {
   if (device < 0 || device >= 64) return HCRC_ERR_NO_DEVICE;
   {

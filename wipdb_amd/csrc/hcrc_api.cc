@@ -491,8 +491,11 @@ int LaunchLong(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const ui
 // long span is the whole job -- run whole, a span's segments are chained on
 // one wave (a lone 1 MiB span: 0.4 ms), split they run on the whole chip
 // (0.07 ms).  Larger batches keep every wave busy with spans of their own
-// (the spans kernel shares long spans over a workgroup's waves).
+// (the spans kernel shares long spans over a workgroup's waves).  A host
+// piece's lengths are known: it takes the split only when one of its spans
+// is long enough to be cut (AutoLongHost).
 constexpr size_t kAutoLongSpans = 16;
+enum class AutoLong { kNo, kDevice };
 
 #ifdef WIPDB_HCRC_TEST_HOOKS
 // Test build only (make testlib, tests/test_gpu_parity.py): with
@@ -522,12 +525,16 @@ int LaunchedLp(hipStream_t st) {
   return rc;
 }
 
-// Descriptor batch on device memory, enqueued on st.
+// Descriptor batch on device memory, enqueued on st.  auto_long: kDevice for
+// the device entry points (a batch of <= kAutoLongSpans spans splits its long
+// spans by itself); host pieces decide on the host (AutoLongHost).
 int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
-                const uint32_t* init, uint32_t* out, size_t count, int flags, hipStream_t st) {
+                const uint32_t* init, uint32_t* out, size_t count, int flags, hipStream_t st,
+                AutoLong auto_long) {
   const bool mask = (flags & HCRC_MASK_OUTPUT) != 0;
   const bool split_long = (flags & HCRC_SPLIT_LONG) != 0 ||
-                          ((flags & HCRC_SPLIT_SMALL) == 0 && count <= kAutoLongSpans);
+                          (auto_long == AutoLong::kDevice && (flags & HCRC_SPLIT_SMALL) == 0 &&
+                           count <= kAutoLongSpans);
   const bool split = !split_long && (flags & HCRC_SPLIT_SMALL) != 0;
   const size_t piece_max = split_long ? size_t(lk::kMaxListSpans) - kDevPartCap
                            : split    ? size_t(lk::kMaxListSpans)
@@ -552,6 +559,17 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
     if (rc) return rc;
   }
   return HCRC_OK;
+}
+
+// A host piece of at most kAutoLongSpans spans with one of >= kDevLongSpan
+// bytes: the long-span split, as a device batch of that size would take.
+// (Spans of >= 256 KiB were already cut into parts on the host,
+// BatchHostLong.)  Other pieces pay for no split.
+int AutoLongHost(const uint32_t* lengths, size_t n) {
+  if (n > kAutoLongSpans) return 0;
+  for (size_t i = 0; i < n; ++i)
+    if (lengths[i] >= kDevLongSpan) return HCRC_SPLIT_LONG;
+  return 0;
 }
 
 // Whether a host piece should go through the size classes: enough spans of
@@ -721,7 +739,9 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
     if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
     rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
-                     flags | AutoSplit(host_base, offsets + i, lengths + i, n), st);
+                     flags | AutoSplit(host_base, offsets + i, lengths + i, n) |
+                         AutoLongHost(lengths + i, n),
+                     st, AutoLong::kNo);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
@@ -771,7 +791,9 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
     if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
     rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
-                     flags | AutoSplit(base, offsets + i, lengths + i, n), st);
+                     flags | AutoSplit(base, offsets + i, lengths + i, n) |
+                         AutoLongHost(lengths + i, n),
+                     st, AutoLong::kNo);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
@@ -1018,7 +1040,7 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const u
     if (rc == HCRC_OK) rc = lane.FaultsBefore();
     if (rc == HCRC_OK)
       rc = LaunchSpans(ctx, base, offsets, lengths, init_crcs, out_crcs, count, flags,
-                       lane->stream);
+                       lane->stream, AutoLong::kDevice);
     if (rc) return rc;
     return lane.CheckFaults();
   }
@@ -1036,7 +1058,7 @@ int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offset
   if (count == 0) return HCRC_OK;
   HCRC_DEVICE(ctx);
   return LaunchSpans(ctx, d_base, d_offsets, d_lengths, d_init_crcs, d_out_crcs, count, flags,
-                     static_cast<hipStream_t>(stream));
+                     static_cast<hipStream_t>(stream), AutoLong::kDevice);
 }
 
 int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride, uint32_t length,
