@@ -10,7 +10,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-PROF_LIB = os.path.join(REPO, "build", "prof", "libhip_crc32c_batch.so")
+PROF_LIB = os.environ.get("WIPDB_PROF_LIB") or os.path.join(REPO, "build", "prof",
+                                                           "libhip_crc32c_batch.so")
 os.environ["WIPDB_HCRC_LIB"] = PROF_LIB
 sys.path.insert(0, REPO)
 

@@ -148,10 +148,29 @@ __device__ __forceinline__ Folded<G> fold(const Lane& k, uint32_t l, uint32_t r)
 // them (the lane's register before them is 0; the span's own register was
 // XORed into its first word).
 __device__ __forceinline__ uint32_t scan(const Lane& k, const uint32_t (&W)[16]) {
+#if defined(WIPDB_LP_SCAN2_EXPERIMENT)
+  // TIMING EXPERIMENT ONLY (wrong results): two independent 8-step chains
+  // (words 0..7, 8..15) joined by a 4-lookup "shift by 32 bytes" that reads
+  // the level-1 tables' bank pattern in place of a real shift table
+  uint32_t x = W[0], y = W[8];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    x = step(k, x, W[i + 1]);
+    y = step(k, y, W[i + 9]);
+  }
+  x = step(k, x, 0u);
+  y = step(k, y, 0u);
+  const uint32_t a0 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[0]));
+  const uint32_t a1 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[1]));
+  const uint32_t a2 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[2]));
+  const uint32_t a3 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[3]));
+  return xor3(a0, a1, a2) ^ a3 ^ y;
+#else
   uint32_t x = W[0];
 #pragma unroll
   for (int i = 0; i < 15; ++i) x = step(k, x, W[i + 1]);
   return step(k, x, 0u);
+#endif
 }
 
 // Sarwate byte step with this lane's copy of T0 (main slot 3).

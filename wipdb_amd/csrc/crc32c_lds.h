@@ -76,7 +76,10 @@ WIPDB_LK_HD constexpr uint32_t MiscAddr(uint32_t i) {
 WIPDB_LK_HD constexpr uint32_t FrontAddr(uint32_t w, uint32_t b) {
   return kLdsFront + 1024u * w + 512u * b;
 }
-constexpr uint32_t kFrontChunks = 32;  // a front piece of at most this many chunks
+#ifndef WIPDB_FRONT_CHUNKS
+#define WIPDB_FRONT_CHUNKS 32
+#endif
+constexpr uint32_t kFrontChunks = WIPDB_FRONT_CHUNKS;  // a front piece of at most this many chunks
 constexpr uint32_t kMiscInvTop = 0;    // 256 words: inv_top[v] (gf2::Tables)
 constexpr uint32_t kMiscHead0 = 256;   // 16 words: ~0 * x^(-8h)
 constexpr uint32_t kMiscUnit = 272;    // the workgroup's unit counter
