@@ -224,16 +224,17 @@ int main(int argc, char** argv) {
     auto in = inits_of(l.size());
     RunSpans("near 4 KiB (inits)", buf, Packed(l, 1, 7), l, &in, false, 3);
   }
-  if (Want(argc, argv, "front edges")) {
-    // front spans (crc32c_plan.h): m segments + a front of 1 .. 32 chunks,
-    // around the 32-chunk limit, odd offsets, inits, both windows in turn
+  if (Want(argc, argv, "small pieces")) {
+    // m segments + 0 .. 36 chunks: segments with back pieces of every
+    // small size (table blocks, ReadBlock's 4 KiB + type + trailer), odd
+    // offsets, inits
     std::vector<uint32_t> l;
     for (uint32_t m = 1; m <= 3; ++m)
       for (uint32_t f = 0; f <= 36; ++f)
         for (uint32_t d = 0; d < 4; ++d) l.push_back(4096u * m + 16u * f - 2u + d);
     auto in = inits_of(l.size());
-    RunSpans("front edges (inits)", buf, Packed(l, 3, 5), l, &in, true, 2);
-    RunVerify("verify front edges", buf, Packed(l, 1, 4), l, 2);
+    RunSpans("segments + small pieces (inits)", buf, Packed(l, 3, 5), l, &in, true, 2);
+    RunVerify("verify segments + small pieces", buf, Packed(l, 1, 4), l, 2);
   }
   if (Want(argc, argv, "long")) {
     auto l = lens_of(300, 8000, 70000);

@@ -53,7 +53,7 @@ uint32_t HeadRegister(uint32_t init, uint32_t h) {
 }
 uint32_t Mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
 
-int g_fail = 0, g_cases = 0, g_pieces = 0, g_segs = 0, g_fronts = 0;
+int g_fail = 0, g_cases = 0, g_pieces = 0, g_segs = 0;
 uint32_t g_max_nl = 0;
 
 struct Case {
@@ -81,69 +81,6 @@ struct Case {
     return &buf[addr - kBase];
   }
 
-  // A front span: the front window (its DMA: window chunk i of 4 nlf reads
-  // span chunk i - (4 nlf - f), the in-front ones and the head chunk 0 read
-  // at c0 + 4 ws), then the segments END-aligned; segment 0's register and
-  // the front's, shifted by 4096 bytes, combine.
-  uint32_t RunFront(const Plan& p, uint32_t residue) {
-    ++g_fronts;
-    const uint32_t f = FrontChunks(p.pw), nlf = (f + 3u) / 4u, nw = 4u * nlf, q0 = nw - f;
-    if (p.m == 0u || f == 0u || f > kFrontChunks || f != (p.C & 255u)) {
-      fprintf(stderr, "  bad front word %#x (C %u, m %u)\n", p.pw, p.C, p.m);
-      ++g_fail;
-      return 0;
-    }
-    std::vector<uint8_t> fw(16u * nw);
-    for (uint32_t i = 0; i < nw; ++i) {
-      const int32_t ci = static_cast<int32_t>(i) - static_cast<int32_t>(q0);
-      const uint64_t off = ci <= 0 ? 4u * p.ws : 16u * static_cast<uint64_t>(ci);
-      memcpy(&fw[16 * i], Read(sbase + p.c0 + off, 16), 16);
-    }
-    memset(fw.data(), 0, 16u * q0);
-    {
-      uint32_t c4[4];
-      memcpy(c4, &fw[16u * q0], 16);
-      fix_head(c4, p.hp, p.ws, HeadRegister(init, p.hp));
-      memcpy(&fw[16u * q0], c4, 16);
-    }
-    const uint32_t RF = Feed(0u, fw.data(), fw.size());
-    uint32_t R = 0;
-    for (uint32_t t = 0; t < p.m; ++t) {
-      ++g_segs;
-      uint8_t win[4096];
-      const uint64_t wb = sbase + p.c0 + 16u * f + 4096u * uint64_t(t);
-      for (uint32_t c = 0; c < 256; ++c) memcpy(win + 16 * c, Read(wb + 16u * c, 16), 16);
-      if (t != 0u) {
-        uint32_t w0;
-        memcpy(&w0, win, 4);
-        w0 ^= R;
-        memcpy(win, &w0, 4);
-      }
-      if (verify && t + 1u == p.m) {
-        uint32_t lo, hi;
-        memcpy(&lo, win + 4088, 4);
-        memcpy(&hi, win + 4092, 4);
-        fix_trailer(lo, hi, p.jv);
-        memcpy(win + 4088, &lo, 4);
-        memcpy(win + 4092, &hi, 4);
-      }
-      R = Feed(0u, win, sizeof(win));
-      if (t == 0u) R ^= FeedZeros(RF, 4096);
-    }
-    if (p.p0 != p.c0 + 16u * uint64_t(p.C)) {
-      fprintf(stderr, "  front span's p0 is not the grid end\n");
-      ++g_fail;
-    }
-    if (p.seg_aux) {
-      const uint8_t* ax = Read(sbase + p.p0 - 12u, 16);
-      R = Feed(R, ax + 12, p.k);
-    } else if (p.k && !verify) {
-      fprintf(stderr, "  a tail but no aux chunk\n");
-      ++g_fail;
-    }
-    return verify ? (R == residue) : ~R;
-  }
-
   // the kernel's result: the CRC (verify: 1 = good block)
   uint32_t Run() {
     const uint64_t end = s_abs + n + (verify ? 4u : 0u);
@@ -152,7 +89,6 @@ struct Case {
     const Plan p = MakePlan(a, static_cast<uint32_t>(s_abs), n, verify);
     if (p.empty) return init;
     const uint32_t residue = verify ? verify_residue(p.jv) : 0u;
-    if (IsFront(p.pw)) return RunFront(p, residue);
     // ---- full segments, from the start ----
     uint32_t R = 0;
     for (uint32_t t = 0; t < p.m; ++t) {
@@ -341,7 +277,7 @@ int main() {
       const uint64_t sbase = (seed >> 33) & 1 ? (s & ~uint64_t(4095)) : B;
       Check(buf, sbase, s, n, init);
     }
-  printf("%s: %d cases, %d pieces (max %u lanes), %d front spans, %d segments, %d failures\n",
-         g_fail ? "FAIL" : "PASS", g_cases, g_pieces, g_max_nl, g_fronts, g_segs, g_fail);
+  printf("%s: %d cases, %d pieces (max %u lanes), %d segments, %d failures\n",
+         g_fail ? "FAIL" : "PASS", g_cases, g_pieces, g_max_nl, g_segs, g_fail);
   return g_fail || g_max_nl != 64u ? 1 : 0;
 }

@@ -39,9 +39,8 @@ struct Lane {
   uint32_t sel[4];  // v_perm selector of lookup j: [K byte j, data byte t_j, 0, 0]
   uint32_t km;      // byte j: 32 t_j + 4 (l & 7)               (main tables)
   uint32_t k1;      // byte j: 128 + 4 (4 a + t_j), a = 7 - l % 8 (fold level 1)
-  uint32_t k2t;     // byte j: 16 t_j (fold level 2: + 64 column, >> 2)
+  uint32_t k2;      // byte j: 8 (4 c + t_j), c = 7 - l / 8     (fold level 2, >> 1)
   uint32_t k1b;     // byte j: 128 + 4 (4 b + t_j), b = 3 - l % 4 (4-lane groups' level 1)
-  uint32_t c2;      // the lane's 8-lane block: shift by 512 c2 bytes at level 2
 };
 
 // G: spans per wave (groups of 64 / G lanes); the level-2 fold shifts the
@@ -51,15 +50,15 @@ __device__ __forceinline__ Lane make_lane(uint32_t l) {
   Lane k;
   constexpr uint32_t LG = 64u / G;
   const uint32_t q = (l >> 3) & 3u, r = l & 7u, a = 7u - (l & 7u);
-  k.c2 = (LG / 8u - 1u) - ((l % LG) >> 3);
-  k.km = k.k1 = k.k2t = k.k1b = 0;
+  const uint32_t c = (LG / 8u - 1u) - ((l % LG) >> 3);
+  k.km = k.k1 = k.k2 = k.k1b = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
     const uint32_t t = (j + q) & 3u;
     k.sel[j] = 0x0c0c0000u | (t << 8) | (4u + j);
     k.km |= (t * 32u + r * 4u) << (8 * j);
     k.k1 |= (128u + (a * 4u + t) * 4u) << (8 * j);
-    k.k2t |= (16u * t) << (8 * j);
+    k.k2 |= (8u * (c * 4u + t)) << (8 * j);
     k.k1b |= (128u + ((3u - (l & 3u)) * 4u + t) * 4u) << (8 * j);
   }
   return k;
@@ -85,30 +84,16 @@ __device__ __forceinline__ uint32_t fold_l1(const Lane& k, uint32_t l, uint32_t 
   return (l & 7u) == 7u ? r : v;
 }
 
-// r * x^(8 * 512 * 2^(col - 1)) mod P: level-2 column col (1, 2, 3 = a
-// shift by 512, 1024, 2048 bytes; crc32c_lds.h)
-__device__ __forceinline__ uint32_t l2_col(const Lane& k, uint32_t col, uint32_t r) {
-  const uint32_t kc = k.k2t + col * 0x40404040u;
-  const uint32_t a0 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[0]) >> 2));
-  const uint32_t a1 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[1]) >> 2));
-  const uint32_t a2 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[2]) >> 2));
-  const uint32_t a3 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[3]) >> 2));
-  return xor3(a0, a1, a2) ^ a3;
-}
-// r * x^(8 * 512 c) mod P for a per-lane c < 2^NB: one level-2 round per bit
-// (no cross-lane operation: callable under a lane branch)
-template <int NB>
-__device__ __forceinline__ uint32_t l2_shift_bits(const Lane& k, uint32_t r, uint32_t c) {
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const uint32_t x = l2_col(k, static_cast<uint32_t>(b) + 1u, r);
-    r = ((c >> b) & 1u) ? x : r;
-  }
-  return r;
-}
-// r * x^(8 * 4096) mod P (two level-2 rounds of 2048 bytes)
-__device__ __forceinline__ uint32_t shift4096(const Lane& k, uint32_t r) {
-  return l2_col(k, 3u, l2_col(k, 3u, r));
+// r * x^(8 * 512 c) mod P (c of make_lane; c = 0: r itself)
+template <int G>
+__device__ __forceinline__ uint32_t fold_l2(const Lane& k, uint32_t l, uint32_t r) {
+  constexpr uint32_t LG = 64u / G;
+  const uint32_t a0 = lds_ld(kLdsL2 + (vperm(k.k2, r, k.sel[0]) >> 1));
+  const uint32_t a1 = lds_ld(kLdsL2 + (vperm(k.k2, r, k.sel[1]) >> 1));
+  const uint32_t a2 = lds_ld(kLdsL2 + (vperm(k.k2, r, k.sel[2]) >> 1));
+  const uint32_t a3 = lds_ld(kLdsL2 + (vperm(k.k2, r, k.sel[3]) >> 1));
+  const uint32_t v = xor3(a0, a1, a2) ^ a3;
+  return ((l % LG) >> 3) == LG / 8u - 1u ? r : v;
 }
 
 template <int G>
@@ -127,8 +112,7 @@ __device__ __forceinline__ Folded<G> fold(const Lane& k, uint32_t l, uint32_t r)
   v ^= dpp<0x4E>(v);   // quad_perm [2,3,0,1]
   v ^= dpp<0x104>(v);  // row_shl:4 -> lanes 8k hold their block of 8
   uint32_t w = 0;
-  // lanes 8k: their block's register by 512 (blocks - 1 - k) bytes
-  if ((l & 7u) == 0u) w = l2_shift_bits<G == 1 ? 3 : (G == 2 ? 2 : 1)>(k, v, k.c2);
+  if ((l & 7u) == 0u) w = fold_l2<G>(k, l, v);
   w ^= dpp<0x108>(w);  // row_shl:8 -> lanes 16k hold their 16
   Folded<G> f;
   if constexpr (G == 1) {
@@ -148,29 +132,10 @@ __device__ __forceinline__ Folded<G> fold(const Lane& k, uint32_t l, uint32_t r)
 // them (the lane's register before them is 0; the span's own register was
 // XORed into its first word).
 __device__ __forceinline__ uint32_t scan(const Lane& k, const uint32_t (&W)[16]) {
-#if defined(WIPDB_LP_SCAN2_EXPERIMENT)
-  // TIMING EXPERIMENT ONLY (wrong results): two independent 8-step chains
-  // (words 0..7, 8..15) joined by a 4-lookup "shift by 32 bytes" that reads
-  // the level-1 tables' bank pattern in place of a real shift table
-  uint32_t x = W[0], y = W[8];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    x = step(k, x, W[i + 1]);
-    y = step(k, y, W[i + 9]);
-  }
-  x = step(k, x, 0u);
-  y = step(k, y, 0u);
-  const uint32_t a0 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[0]));
-  const uint32_t a1 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[1]));
-  const uint32_t a2 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[2]));
-  const uint32_t a3 = lds_ld(kLdsMain + vperm(k.k1, x, k.sel[3]));
-  return xor3(a0, a1, a2) ^ a3 ^ y;
-#else
   uint32_t x = W[0];
 #pragma unroll
   for (int i = 0; i < 15; ++i) x = step(k, x, W[i + 1]);
   return step(k, x, 0u);
-#endif
 }
 
 // Sarwate byte step with this lane's copy of T0 (main slot 3).
@@ -435,6 +400,23 @@ __device__ __forceinline__ uint32_t fold4(const Lane& k, uint32_t l, uint32_t r)
   v ^= dpp<0xB1>(v);  // quad_perm [1,0,3,2]
   v ^= dpp<0x4E>(v);  // quad_perm [2,3,0,1]
   return v;
+}
+
+// r * x^(8 * 512 c) mod P from the level-2 tables, for any lane (kc: the
+// lane's selector constant for column c, make_l2c).
+__device__ __forceinline__ uint32_t l2_shift(const Lane& k, uint32_t kc, uint32_t r) {
+  const uint32_t a0 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[0]) >> 1));
+  const uint32_t a1 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[1]) >> 1));
+  const uint32_t a2 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[2]) >> 1));
+  const uint32_t a3 = lds_ld(kLdsL2 + (vperm(kc, r, k.sel[3]) >> 1));
+  return xor3(a0, a1, a2) ^ a3;
+}
+__device__ __forceinline__ uint32_t make_l2c(uint32_t l, uint32_t c) {
+  const uint32_t q = (l >> 3) & 3u;
+  uint32_t kc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) kc |= (8u * (c * 4u + ((j + q) & 3u))) << (8 * j);
+  return kc;
 }
 
 __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t lane) {

@@ -4,16 +4,10 @@
 //
 // One 1024-thread workgroup (16 waves) per CU owns all 160 KiB of LDS:
 //
-//   [0, 16 KiB)     fold level-2 tables, 256 rows of 64 B: row b holds
-//                   entry (col, p) at 16 col + 4 p = shift(b << 8p, 512 *
-//                   2^(col - 1) bytes) for col = 1, 2, 3 (512, 1024, 2048
-//                   bytes: a shift by 512 c is one round per bit of c); the
-//                   col = 0 column (bytes 0..15 of each row) holds the misc
-//                   words.
-//   [16, 32 KiB)    front windows: wave w's two of 512 B at 16 KiB + 1 KiB w,
-//                   the front piece DMA'd in with a span's first segment
-//                   (run_lp: spans of m segments + a front of <= 32 chunks),
-//                   alternating.
+//   [0, 32 KiB)     fold level-2 tables, 256 rows of 128 B: row b holds
+//                   entry (c, p) at (4c + p) * 4 = shift(b << 8p, 512c bytes)
+//                   for c = 1..7; the c = 0 column (bytes 0..15 of each row,
+//                   an identity shift nobody looks up) holds the misc words.
 //   [32, 96 KiB)    main region, 256 rows of 256 B:
 //                   bytes [0, 128): slicing-by-4 tables, slot t (0..3) x
 //                   replica r (0..7) at 32t + 4r = T[3 - t][b] (the table of
@@ -30,9 +24,8 @@
 // bank = (address / 4) mod 32).  In lookup instruction j a lane reads the
 // table slot t = (j + q) & 3, q = (lane >> 3) & 3, replica r = lane & 7:
 // the 32 lanes of a half hit banks 8t + r -- all different, for any data.
-// The level-1 fold reads column 4a + t with a = 7 - (lane & 7): distinct
-// banks again; the level-2 rounds run on lanes 8k only (the fold) or on
-// pieces' lanes (shift64).
+// The level-1 fold reads column 4a + t with a = 7 - (lane & 7), the
+// level-2 fold (lanes 8k only) column 4c + t: distinct banks again.
 // Each lookup address is ONE v_perm_b32 of (lane constant, data word,
 // per-lane selector): [const byte j, data byte t, 0, 0] = (byte << 8) | const.
 #pragma once
@@ -52,7 +45,6 @@ namespace lk {
 constexpr int kWaves = 16;
 constexpr int kThreads = kWaves * 64;
 constexpr uint32_t kLdsL2 = 0;
-constexpr uint32_t kLdsFront = 16384;
 constexpr uint32_t kLdsMain = 32768;
 constexpr uint32_t kLdsSlots = 98304;
 constexpr uint32_t kSlotBytes = 4096;
@@ -67,19 +59,10 @@ WIPDB_LK_HD constexpr uint32_t AuxAddr(uint32_t w, uint32_t k) {
 constexpr uint32_t kAuxTail = 0;   // + g (g < 8): group g's tail chunk
 constexpr uint32_t kAuxNext = 8;   // + g: the chunk after it (verify trailers)
 
-// misc word i (i < 1024) lives in the col = 0 column of level-2 row i / 4
+// misc word i (i < 1024) lives in the c = 0 column of level-2 row i / 4
 WIPDB_LK_HD constexpr uint32_t MiscAddr(uint32_t i) {
-  return (i >> 2) * 64u + (i & 3u) * 4u;
+  return (i >> 2) * 128u + (i & 3u) * 4u;
 }
-// wave w's front windows: two of 512 B (b = 0, 1), so the next span's front
-// may land while this one's is still to be read (crc32c_plan.h front spans)
-WIPDB_LK_HD constexpr uint32_t FrontAddr(uint32_t w, uint32_t b) {
-  return kLdsFront + 1024u * w + 512u * b;
-}
-#ifndef WIPDB_FRONT_CHUNKS
-#define WIPDB_FRONT_CHUNKS 32
-#endif
-constexpr uint32_t kFrontChunks = WIPDB_FRONT_CHUNKS;  // a front piece of at most this many chunks
 constexpr uint32_t kMiscInvTop = 0;    // 256 words: inv_top[v] (gf2::Tables)
 constexpr uint32_t kMiscHead0 = 256;   // 16 words: ~0 * x^(-8h)
 constexpr uint32_t kMiscUnit = 272;    // the workgroup's unit counter
@@ -99,13 +82,13 @@ constexpr uint32_t kMiscBytes = 1024 * 4;
 //     keep their aux pieces there instead): {a_lo, a_hi, n, span + 1}, a
 //     last word of 0 = a free slot; record k's init_crc in misc word
 //     kMiscQInit + k;
-//   * wave w's aux chunk of a segment tail: the col = 0 column of level-2 row
-//     128 + w (misc words 512 + 4 w ..).
+//   * wave w's aux chunk of a segment tail: the c = 0 column of level-2 row
+//     128 + w (misc words 512.. are unused).
 constexpr uint32_t kQSlots = 256;
 WIPDB_LK_HD constexpr uint32_t QRecAddr(uint32_t k) {
   return kLdsMain + (k & (kQSlots - 1u)) * 256u + 128u;
 }
-WIPDB_LK_HD constexpr uint32_t SegAuxAddr(uint32_t w) { return kLdsL2 + (128u + w) * 64u; }
+WIPDB_LK_HD constexpr uint32_t SegAuxAddr(uint32_t w) { return kLdsL2 + (128u + w) * 128u; }
 
 // Flags of a launch (the HCRC_MASK_OUTPUT value is shared with the C-ABI).
 constexpr uint32_t kFlagMask = 0x2;
@@ -141,10 +124,10 @@ inline void BuildLdsImage(uint32_t* img) {
   BuildTables(&T);
   for (uint32_t i = 0; i < kImageBytes / 4; ++i) img[i] = 0;
   uint32_t sh[4][256];
-  for (int col = 1; col <= 3; ++col) {
-    BuildShiftTable(uint64_t(512) << (col - 1), sh);
+  for (int c = 1; c < 8; ++c) {
+    BuildShiftTable(uint64_t(512) * c, sh);
     for (int p = 0; p < 4; ++p)
-      for (int b = 0; b < 256; ++b) img[(kLdsL2 + b * 64 + col * 16 + p * 4) / 4] = sh[p][b];
+      for (int b = 0; b < 256; ++b) img[(kLdsL2 + b * 128 + (c * 4 + p) * 4) / 4] = sh[p][b];
   }
   for (int b = 0; b < 256; ++b)
     for (int t = 0; t < 4; ++t)

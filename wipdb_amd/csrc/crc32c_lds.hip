@@ -114,24 +114,23 @@ __device__ __forceinline__ uint32_t scan_or(uint32_t v) {  // the OR of the wave
 }
 
 // r * x^(8 * 64 d) mod P for a per-lane d in [0, 63]: level-1 tables (64 a
-// bytes, a = d % 8) then the level-2 rounds (512, 1024, 2048 bytes: the bits
-// of c = d / 8; a round no lane needs is skipped -- pieces of <= 8 lanes
-// need none).  k1b: the lane's level-1 selector base (bytes 128 + 4 t_j,
-// crc32c_lds.h).  All lanes call it.
-__device__ __forceinline__ uint32_t shift64(const Lane& k, uint32_t k1b, uint32_t r, uint32_t d) {
+// bytes, a = d % 8) then level-2 tables (512 c bytes, c = d / 8).  k1b / k2b:
+// the lane's selector bases (bytes 128 + 4 t_j / 8 t_j, crc32c_lds.h).
+__device__ __forceinline__ uint32_t shift64(const Lane& k, uint32_t k1b, uint32_t k2b, uint32_t r,
+                                            uint32_t d) {
   const uint32_t a = d & 7u, c = (d >> 3) & 7u;
   const uint32_t k1 = k1b + a * 0x10101010u;
   const uint32_t a0 = lds_ld(kLdsMain + vperm(k1, r, k.sel[0]));
   const uint32_t a1 = lds_ld(kLdsMain + vperm(k1, r, k.sel[1]));
   const uint32_t a2 = lds_ld(kLdsMain + vperm(k1, r, k.sel[2]));
   const uint32_t a3 = lds_ld(kLdsMain + vperm(k1, r, k.sel[3]));
-  uint32_t v = vsel(ballot(a != 0u), xor3(a0, a1, a2) ^ a3, r);
-#pragma unroll
-  for (uint32_t b = 0; b < 3; ++b) {
-    const uint64_t m = ballot(((c >> b) & 1u) != 0u);
-    if (m != 0u) v = vsel(m, l2_col(k, b + 1u, v), v);
-  }
-  return v;
+  const uint32_t v = a != 0u ? (xor3(a0, a1, a2) ^ a3) : r;
+  const uint32_t k2 = k2b + c * 0x20202020u;
+  const uint32_t b0 = lds_ld(kLdsL2 + (vperm(k2, v, k.sel[0]) >> 1));
+  const uint32_t b1 = lds_ld(kLdsL2 + (vperm(k2, v, k.sel[1]) >> 1));
+  const uint32_t b2 = lds_ld(kLdsL2 + (vperm(k2, v, k.sel[2]) >> 1));
+  const uint32_t b3 = lds_ld(kLdsL2 + (vperm(k2, v, k.sel[3]) >> 1));
+  return c != 0u ? (xor3(b0, b1, b2) ^ b3) : v;
 }
 
 // ~init * x^(-8 h) per lane (head_register is the uniform form).
@@ -202,15 +201,12 @@ __device__ __forceinline__ Stripe make_stripe_v(PW pw, uint32_t j) {
 }
 
 // A segment iteration (uniform).
-// kSFirst: segment 0 of a span with its head; kSFront: segment 0 of a front
-// span, its front piece in front window kSFrontB (crc32c_plan.h)
-constexpr uint32_t kSFirst = 1u, kSLast = 2u, kSPush = 4u, kSAux = 8u, kSFront = 16u,
-                   kSFrontB = 32u;
+constexpr uint32_t kSFirst = 1u, kSLast = 2u, kSPush = 4u, kSAux = 8u;
 struct SegW {
   uint32_t fl;
   uint32_t hw;    // hp | ws << 4 | k << 6 | jv << 8
   uint32_t init, id;
-  uint32_t pw;    // kSPush: the back piece's word; kSFront: the front word
+  uint32_t pw;    // kSPush: the back piece's word
   uint64_t p0;    // kSPush: its first chunk (offset from the source base)
 };
 // What an iteration computes.
@@ -260,11 +256,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
 
   // per-lane selector bases of the batch fold (shift64) and the batch DMA's
   // stripe / chunk of this lane in each of its 4 instructions
-  uint32_t k1b = 0;
+  uint32_t k1b = 0, k2b = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
     const uint32_t t = (j + ((l >> 3) & 3u)) & 3u;
     k1b |= (128u + 4u * t) << (8 * j);
+    k2b |= (8u * t) << (8 * j);
   }
   const uint32_t dsl = l >> 2;                          // stripe lane 16 q + dsl
   const uint32_t dci = ((l & 3u) - (l >> 4)) & 3u;      // chunk of that stripe
@@ -302,7 +299,6 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t nb_pw = 0, nb_inj = 0, nb_id = 0, nb_j = 0;
   uint32_t carry = 0, carry_tw = 0;   // the split piece's register over its first lanes, tail word
   uint32_t chain = 0;
-  uint32_t fbuf = 0;  // the front window the next front DMA fills (0 / 1)
 
   // The workgroup's units: unit u is span ((u / 16) * grid + wg) * 16 +
   // u % 16 -- blocks of 16 spans round robin over the grid, so the chip
@@ -564,32 +560,17 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // ---- decide: issue the next iteration's DMA ----
   auto issue_seg = [&]() {
     const uint32_t m = PL_m(lpl);
-    const bool front = lt == 0u && IsFront(lpw);
-    const uint32_t f = IsFront(lpw) ? FrontChunks(lpw) : 0u;
-    // the back piece / the grid end (front spans: segments END-aligned after
-    // the front's f chunks)
-    const uint64_t p0 = lc0 + 16u * f + 4096u * static_cast<uint64_t>(m);
-    const uint64_t wb = sbase + lc0 + 16u * f + 4096u * static_cast<uint64_t>(lt);
+    const uint64_t p0 = lc0 + 4096u * static_cast<uint64_t>(m);  // the back piece / span grid end
+    const uint64_t wb = sbase + lc0 + 4096u * static_cast<uint64_t>(lt);
     const uint32_t o = 16u * pp.cm;
-    const uint32_t s0 = lt == 0u && f == 0u ? 4u * PL_ws(lpl) : 0u;
+    const uint32_t s0 = lt == 0u ? 4u * PL_ws(lpl) : 0u;
     dma4(wb, pp.slot, o > s0 ? o : s0, o + 1024u, o + 2048u, o + 3072u);
-    if (front) {
-      // the front piece: window chunk i of 4 nlf (lane i) reads span chunk
-      // i - (4 nlf - f); the in-front chunks and the head chunk 0 read at
-      // c0 + 4 ws (chunk 0 ws words late: page-safe, crc32c_plan.h)
-      const uint32_t nw = 4u * ((f + 3u) >> 2);
-      const int32_t ci = static_cast<int32_t>(l) - static_cast<int32_t>(nw - f);
-      const uint32_t off = ci <= 0 ? 4u * PL_ws(lpl) : 16u * static_cast<uint32_t>(ci);
-      if (l < nw) dma1nt(sbase + lc0, FrontAddr(w, fbuf), off);
-    }
     const bool last = lt + 1u == m;
     const bool aux = last && PL_aux(lpl) != 0u;
-    ns.fl = (lt == 0u && f == 0u ? kSFirst : 0u) | (last ? kSLast : 0u) |
-            (last && lpw != 0u && f == 0u ? kSPush : 0u) | (aux ? kSAux : 0u) |
-            (front ? kSFront | (fbuf ? kSFrontB : 0u) : 0u);
-    if (front) fbuf ^= 1u;
-    // (seg_aux: no piece, so the grid ends at p0; the aux chunk is the 16
-    // bytes ending at E4 + 4)
+    ns.fl = (lt == 0u ? kSFirst : 0u) | (last ? kSLast : 0u) |
+            (last && lpw != 0u ? kSPush : 0u) | (aux ? kSAux : 0u);
+    // (seg_aux: no piece, so the grid ends at c0 + 4096 m; the aux chunk is
+    // the 16 bytes ending at E4 + 4)
     if (aux) dma_piece(l, sbase + p0 - 12u, 0u, SegAuxAddr(w));
     ns.hw = PL_hw(lpl);
     ns.init = linit;
@@ -736,8 +717,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
           const uint32_t inj = (c.init | hp) == 0u ? ~0u : head_register(l, c.init, hp);
           if ((hp | ws) == 0u) h4[0] ^= inj;
           else fix_head(h4, hp, ws, inj);
-        } else if (!(c.fl & kSFront)) {
-          h4[0] ^= chain;  // (a front span's segment 0 starts from 0: the front joins after)
+        } else {
+          h4[0] ^= chain;
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) W[i] = l == 0u ? h4[i] : W[i];
@@ -748,53 +729,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
         W[14] = l == 63u ? lo : W[14];
         W[15] = l == 63u ? hi : W[15];
       }
-      uint32_t Rl = scan(lk, W);
-      if (c.fl & kSFront) {
-        // the front piece, from the front window: window stripe j on lane
-        // 64 - nlf + j (END-aligned at lane 63, so the fold shifts it right),
-        // in-front chunks zeroed, the head chunk in span form with the head
-        // register; its lanes' registers shifted by the segment's 4096 bytes
-        // join the segment's before the fold (shifts commute)
-        const uint32_t f = FrontChunks(c.pw), nlf = (f + 3u) >> 2, q0 = 4u * nlf - f;
-        const uint32_t inj = (c.init | hp) == 0u ? ~0u : head_register(l, c.init, hp);
-        if (l >= 64u - nlf) {
-          const uint32_t j = l - (64u - nlf);
-          const uint32_t fa = FrontAddr(w, (c.fl & kSFrontB) ? 1u : 0u) + 64u * j;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const u32x4 d = lds_ld4(fa + 16u * static_cast<uint32_t>(i));
-            W[4 * i] = d.x;
-            W[4 * i + 1] = d.y;
-            W[4 * i + 2] = d.z;
-            W[4 * i + 3] = d.w;
-          }
-          if (j == 0u) {
-            uint32_t h4[4] = {W[0], W[1], W[2], W[3]};
-            // chunk q0 (< 4) is the head; the ones in front of it are zeroed
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint32_t qi = static_cast<uint32_t>(i);
-              if (qi == q0) {
-                uint32_t cq[4] = {W[4 * i], W[4 * i + 1], W[4 * i + 2], W[4 * i + 3]};
-                fix_head(cq, hp, ws, inj);
-                h4[0] = cq[0];
-                h4[1] = cq[1];
-                h4[2] = cq[2];
-                h4[3] = cq[3];
-              }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint32_t qi = static_cast<uint32_t>(i);
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                W[4 * i + q] = qi < q0 ? 0u : (qi == q0 ? h4[q] : W[4 * i + q]);
-            }
-          }
-          Rl ^= shift4096(lk, scan(lk, W));
-        }
-      }
-      uint32_t R = fold<1>(lk, l, Rl)[0];
+      uint32_t R = fold<1>(lk, l, scan(lk, W))[0];
       if (!(c.fl & kSLast)) {
         chain = R;
         return false;
@@ -984,7 +919,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       }
       const uint32_t R = scan(lk, W);
       const uint32_t d = live ? nl - 1u - j : 0u;  // lanes of the piece after this one
-      const uint32_t v = shift64(lk, k1b, R, d);
+      const uint32_t v = shift64(lk, k1b, k2b, R, d);
       const uint32_t xs = scan_xor(v);
       // the piece's lanes in this batch end at lane l + min(d, 63 - l): the
       // XOR over them, at its first lane here (j == j0)

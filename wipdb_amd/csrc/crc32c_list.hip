@@ -237,7 +237,7 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
         // register after piece || main = rp * x^(8 * 4096) ^ main register;
         // then the tail
         // (verify: T holds the residue, and there is no tail)
-        const uint32_t sft = shift4096(lk, rp);
+        const uint32_t sft = l2_shift(lk, make_l2c(l, 1u), l2_shift(lk, make_l2c(l, 7u), rp));
         if (kVerify) {
           out8[sid] = sft == T ? 1u : 0u;
         } else {

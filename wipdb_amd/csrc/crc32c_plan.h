@@ -20,19 +20,9 @@
 // 4-byte boundary (jv <= 3 bytes past it) and the trailer is checked through
 // the CRC residue (fix_trailer / verify_residue).
 //
-// The plan.  m = C / 256 full segments, r = C mod 256 chunks left over.
-//
-// FRONT spans (m >= 1, 1 <= r <= kFrontChunks: table blocks, ReadBlock's
-// 4 KiB + type byte + trailer, ...): the r chunks go FIRST, as a front piece
-// DMA'd with segment 0 into the wave's front window, and the segments follow
-// END-aligned (segment t = chunks [r + 256 t, r + 256 t + 256)).  Segment 0's
-// iteration checksums both: the front (head included) on the last ceil(r / 4)
-// lanes, its register shifted by 4096 bytes and folded in with the segment's
-// (crc32c_lds.hip seg_compute) -- one iteration, no piece in the ring.
-//
-// Other spans: m full segments FROM THE START of the grid (segment t
+// The plan.  m = C / 256 full segments FROM THE START of the grid (segment t
 // = chunks [256 t, 256 t + 256), one wave iteration each, chained by the
-// register; segment 0 carries the head), then a BACK PIECE of r
+// register; segment 0 carries the head), then a BACK PIECE of r = C mod 256
 // chunks (a span of fewer than 256 chunks is all piece, head included).  A
 // piece does not get a 4 KiB window of its own: pieces queue in the wave's
 // piece ring and one wave iteration checksums as many of them as fit in its
@@ -77,10 +67,6 @@ WIPDB_LK_HD inline uint32_t head_mask(uint32_t h, uint32_t ww) {
 // j0: the kernel split the piece over two batch iterations and lanes
 // [j0, nl) of it are still to come (the register of lanes [0, j0) is carried).
 constexpr uint32_t kPWCont = 1u << 23;
-// A front span's word instead (no back piece): kPWFront | r, the front's chunks.
-constexpr uint32_t kPWFront = 1u << 31;
-WIPDB_LK_HD inline bool IsFront(uint32_t pw) { return (pw & kPWFront) != 0u; }
-WIPDB_LK_HD inline uint32_t FrontChunks(uint32_t pw) { return pw & 0xffu; }
 struct PW {
   uint32_t v;
   WIPDB_LK_HD inline uint32_t r() const { return v & 0xffu; }
@@ -109,12 +95,11 @@ WIPDB_LK_HD inline uint32_t PackPW(uint32_t r, uint32_t x, uint32_t hp, uint32_t
 // The plan of one span.
 struct Plan {
   uint64_t c0;    // offset (from the source base) of grid chunk 0 (= s - hp)
-  uint64_t p0;    // offset of the piece's first chunk (c0 + 4096 m = E4 - 16 r; a front
-                  // span: the grid's end, c0 + 16 C)
+  uint64_t p0;    // offset of the piece's first chunk (c0 + 4096 m = E4 - 16 r)
   uint32_t C;     // body chunks
   uint32_t m;     // full segments
   uint32_t hp, ws, k, jv;
-  uint32_t pw;    // the piece word (0: no piece; kPWFront | r: a front span)
+  uint32_t pw;    // the piece word (0: no piece)
   uint32_t seg_aux;  // m > 0, no piece, a tail: the last segment reads the aux chunk at c0 + 16 C - 12
   bool empty;     // a CRC span of 0 bytes: out = init, nothing read
 };
@@ -152,12 +137,8 @@ WIPDB_LK_HD inline Plan MakePlan(uint64_t a, uint32_t s_lo, uint32_t n, bool ver
   const uint32_t r = C & 255u;
   p.p0 = p.c0 + 4096u * static_cast<uint64_t>(p.m);
   p.pw = 0;
-  if (p.m != 0u && r <= kFrontChunks) {
+  if (p.m != 0u && r == 0u) {
     p.seg_aux = k != 0u ? 1u : 0u;  // aux chunk: c0 + 16 C - 12 (16 bytes ending at E4 + 4)
-    if (r != 0u) {
-      p.pw = kPWFront | r;
-      p.p0 += 16u * r;
-    }
     return p;
   }
   if (p.empty) return p;
