@@ -80,10 +80,11 @@ extern "C" {
 #define HCRC_MASK_OUTPUT 0x2  /* write Mask(crc) instead of crc             */
 /* Size classes: a partition pass sorts the batch into spans of at most
  * ~1 KiB (checksummed 4 per wave iteration), at most ~2 KiB (2 per wave
- * iteration) and longer ones (the spans kernel's pipeline).  Same results;
- * pays off for batches with many short spans (WAL records, small meta
- * blocks).  hcrc_batch on host memory chooses it by itself.  Uses
- * stream-ordered scratch (~60 bytes per span). */
+ * iteration) and longer ones (round 2's end-aligned pipeline).  Same results.
+ * An opt-in: the default kernel packs short spans by itself and is as fast or
+ * faster on every measured shape, so no entry point
+ * chooses it by itself any more.  Uses stream-ordered scratch (~60 bytes per
+ * span). */
 #define HCRC_SPLIT_SMALL 0x4
 /* Long spans (device batches; host batches do it by themselves for spans of
  * >= 256 KiB): a span of >= 128 KiB is cut into 16 KiB parts checksummed on

@@ -158,7 +158,8 @@ def test_split_small_boundaries_and_mix(engine, oracle):
     inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
     want = oracle.batch(buf, offs, lens, inits)
     np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits, split=True), want)
-    # host path: chooses the split by itself (>= 256 small spans)
+    # host path: the default kernel (no entry point picks the classes by
+    # itself since round 4: profiles/r04c_autosplit_ab.log)
     np.testing.assert_array_equal(engine.batch(buf, offs, lens, inits), want)
 
 
@@ -188,7 +189,7 @@ def test_split_remainders(engine, oracle):
     np.testing.assert_array_equal(
         _run_device(engine, buf, offs, lens, inits, mask=True, split=True),
         np.array([oracle.lib.oracle_mask(int(x)) for x in want], np.uint32))
-    # SST-packed table blocks (contents + type byte), host path (auto split)
+    # SST-packed table blocks (contents + type byte), host path
     blens, boffs, cur = [], [], 0
     while cur + 4300 < buf.size // 4:
         n = int(rng.integers(4097, 4226))

@@ -572,29 +572,24 @@ int AutoLongHost(const uint32_t* lengths, size_t n) {
   return 0;
 }
 
-// Whether a host piece should go through the size classes: enough spans of
-// at most ~1.25 KiB (WAL records, small meta blocks) to pay for the
-// partition pass and the two extra launches.  Larger spans run as fast or
-// faster on the spans kernel (config 3, profiles/r02d_extra*.log: 2 KiB
-// spans 3186 GiB/s unsplit vs 2891 split; 1 KiB spans 1592 vs 2602), and
-// table blocks -- 4 KiB plus their last entry -- need no classes at all.
-// Span i's address mod 16 is base + offsets[i]'s.
-constexpr size_t kAutoSplitMin = 256;
-constexpr uint32_t kAutoSplitChunks = 80;
+// Whether a host piece goes through the size classes (HCRC_SPLIT_SMALL) by
+// itself: no longer.  Round 2 chose them for pieces of >= 256 short spans;
+// on round 3's lane-packed kernel they lose everywhere (same session,
+// profiles/r04c_autosplit_ab.log: WAL records, meta blocks, 512 B and 1 KiB
+// spans, 4 and 32 MiB batches -- device-resident 2-2.7x slower, zero-copy up
+// to 17 % slower, staged within 4 % either way), so the default kernel runs
+// every host piece; the classes stay an opt-in flag.
 int AutoSplit(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, size_t n) {
+  (void)base;
+  (void)offsets;
+  (void)lengths;
+  (void)n;
 #ifdef WIPDB_HCRC_TEST_HOOKS
-  // A/B of the choice itself (scripts/autosplit_ab.py): "0" never, "1" always
-  if (const char* e = getenv("WIPDB_HCRC_AUTOSPLIT")) {
-    if (*e == '0') return 0;
+  // the A/B of the choice (scripts/autosplit_ab.py): "1" forces the classes
+  if (const char* e = getenv("WIPDB_HCRC_AUTOSPLIT"))
     if (*e == '1') return HCRC_SPLIT_SMALL;
-  }
 #endif
-  size_t hits = 0;
-  for (size_t i = 0; i < n && hits < kAutoSplitMin; ++i) {
-    const uint32_t h = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(base) + offsets[i]) & 15u);
-    hits += ((h + lengths[i]) >> 4) <= kAutoSplitChunks;
-  }
-  return hits >= kAutoSplitMin ? HCRC_SPLIT_SMALL : 0;
+  return 0;
 }
 
 // Persistent helper threads for the pageable -> pinned staging copy (the
