@@ -42,7 +42,10 @@
 namespace wipdb {
 namespace lk {
 
-constexpr int kWaves = 16;
+#ifndef WIPDB_LP_WAVES
+#define WIPDB_LP_WAVES 16
+#endif
+constexpr int kWaves = WIPDB_LP_WAVES;  // waves per workgroup (one workgroup per CU)
 constexpr int kThreads = kWaves * 64;
 constexpr uint32_t kLdsL2 = 0;
 constexpr uint32_t kLdsMain = 32768;
