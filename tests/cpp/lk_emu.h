@@ -159,6 +159,18 @@ inline std::atomic<uint32_t> g_hide_marker{~0u};
 inline std::atomic<uint32_t> g_spin{1u << 22};  // WIPDB_LP_SPIN of the emulation
 }
 inline uint32_t queue_marker(uint32_t v, uint32_t idx) { return idx == emu::g_hide_marker.load() ? 0u : v; }
+// the launches' pipeline choices (bit 0 run_ea, bit 1 run_lp); g_force_pipe
+// >= 0 overrides the choice (1 = run_ea, 0 = run_lp)
+namespace emu {
+inline std::atomic<uint32_t> g_pipes{0};
+inline std::atomic<int> g_force_pipe{-1};
+}
+inline bool pipeline_marker(bool ea) {
+  const int f = emu::g_force_pipe.load();
+  if (f >= 0) ea = f != 0;
+  emu::g_pipes.fetch_or(ea ? 1u : 2u);
+  return ea;
+}
 
 // ---- lanes ----
 inline uint32_t lane_tid() { return emu::t_tid; }

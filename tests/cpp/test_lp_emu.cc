@@ -10,7 +10,7 @@
 // The queue's timeout path is forced once (a hidden record marker and a small
 // spin bound): the launch must report the fault.
 // Build: clang++ -std=c++17 -O1 -pthread -I wipdb_amd/csrc -I tests/cpp.
-// Usage: test_lp_emu [case ...]; exit 0 = pass.
+// Usage: test_lp_emu [--pipe=ea|lp] [case ...]; exit 0 = pass.
 #define WIPDB_LK_EMU 1
 // the queue's spin bound, set per case (run-time in the emulation)
 #define WIPDB_LP_SPIN (::wipdb::lk::emu::g_spin.load())
@@ -38,6 +38,8 @@ uint32_t Extend(uint32_t init, const uint8_t* p, size_t n) {
 }
 
 int g_fail = 0;
+// the pipeline the next launches must choose (1 run_ea, 2 run_lp, 0 any)
+uint32_t g_want_pipe = 0;
 
 // DMA sources must lie in the pages of the buffer (the kernel's guarantee:
 // nothing outside the pages that hold bytes of a span is read)
@@ -67,8 +69,14 @@ void Report(const char* name, const std::vector<uint32_t>& got, const std::vecto
   if (bs) fprintf(stderr, "  %s: DMA source %#llx outside the buffer\n", name, (unsigned long long)(bs & ~1ull));
   const uint32_t fb = emu::g_faults.exchange(0);
   if (fb) fprintf(stderr, "  %s: the launch reported fault bits %#x\n", name, fb);
-  printf("%-34s %6zu spans  %s (%zu bad)\n", name, want.size(), bad || bs || fb ? "FAIL" : "ok", bad);
-  if (bad || bs || fb) ++g_fail;
+  const uint32_t pipes = emu::g_pipes.exchange(0);
+  const bool pipe_bad =
+      pipes == 3u || (g_want_pipe != 0u && emu::g_force_pipe.load() < 0 && pipes != g_want_pipe);
+  if (pipe_bad) fprintf(stderr, "  %s: pipelines %#x, want %#x\n", name, pipes, g_want_pipe);
+  const bool fail = bad || bs || fb || pipe_bad;
+  printf("%-34s %6zu spans  %s %s (%zu bad)\n", name, want.size(), pipes == 1u ? "ea" : "lp",
+         fail ? "FAIL" : "ok", bad);
+  if (fail) ++g_fail;
 }
 
 // CRC batch through crc32c_lds_spans_kernel
@@ -151,15 +159,24 @@ std::vector<uint64_t> Packed(const std::vector<uint32_t>& lens, uint64_t start, 
 }
 
 bool Want(int argc, char** argv, const char* name) {
-  if (argc < 2) return true;
-  for (int i = 1; i < argc; ++i)
+  bool any = false;
+  for (int i = 1; i < argc; ++i) {
+    if (argv[i][0] == '-') continue;
+    any = true;
     if (strstr(name, argv[i])) return true;
-  return false;
+  }
+  return !any;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
+  // --pipe=ea / --pipe=lp: every launch takes that pipeline (both must be
+  // exact on every shape; the choice only changes speed)
+  for (int i = 1; i < argc; ++i) {
+    if (!strcmp(argv[i], "--pipe=ea")) emu::g_force_pipe = 1;
+    if (!strcmp(argv[i], "--pipe=lp")) emu::g_force_pipe = 0;
+  }
   wipdb::gf2::BuildTables(&T);
   BuildLdsImage(g_image.data());
   std::mt19937_64 rng(7);
@@ -213,11 +230,15 @@ int main(int argc, char** argv) {
   if (Want(argc, argv, "aligned 4 KiB")) {
     std::vector<uint64_t> o;
     for (int i = 0; i < 2000; ++i) o.push_back(4096u * i);
+    g_want_pipe = 1;
     RunSpans("aligned 4 KiB", buf, o, std::vector<uint32_t>(2000, 4096), nullptr, false, 3);
+    g_want_pipe = 0;
   }
   if (Want(argc, argv, "table blocks")) {
     auto l = lens_of(2000, 4097, 4225);
+    g_want_pipe = 1;
     RunSpans("table blocks", buf, Packed(l, 0, 4), l, nullptr, true, 3);
+    g_want_pipe = 0;
   }
   if (Want(argc, argv, "near 4 KiB")) {
     auto l = lens_of(2000, 3960, 4240);
@@ -238,7 +259,13 @@ int main(int argc, char** argv) {
   }
   if (Want(argc, argv, "long")) {
     auto l = lens_of(300, 8000, 70000);
+    g_want_pipe = 2;
     RunSpans("long 8..70 KiB", buf, Packed(l, 2, 5), l, nullptr, false, 2);
+    auto l2 = lens_of(120, 32768, 200000);
+    auto in2 = inits_of(l2.size());
+    g_want_pipe = 1;
+    RunSpans("long 32..200 KiB (inits)", buf, Packed(l2, 5, 3), l2, &in2, true, 2);
+    g_want_pipe = 0;
   }
   if (Want(argc, argv, "shared long")) {  // one wave's desks of long spans, the others idle: shared
     auto l = lens_of(16, 20000, 70000);
@@ -296,16 +323,22 @@ int main(int argc, char** argv) {
       }
       l.push_back(B[k] + static_cast<uint32_t>(rng() % (B[k] / 8 + 1)));
     }
+    g_want_pipe = 2;
     RunSpans("zipf mix", buf, Packed(l, 3, 5), l, nullptr, false, 4);
+    g_want_pipe = 0;
   }
   if (Want(argc, argv, "verify")) {
     auto l = lens_of(1500, 1, 5000);
     RunVerify("verify mixed", buf, Packed(l, 9, 4), l, 3);
     auto l2 = lens_of(1000, 4096, 4225);
+    g_want_pipe = 1;
     RunVerify("verify table blocks", buf, Packed(l2, 0, 4), l2, 3);
+    g_want_pipe = 0;
   }
   if (Want(argc, argv, "strided")) {
+    g_want_pipe = 1;
     RunStrided("strided 4096", buf, 4096, 4096, 0, 1500, 3);
+    g_want_pipe = 0;
     RunStrided("strided 700 / 513 (init)", buf, 700, 513, 0x12345678u, 1500, 2);
     RunStrided("strided 4096 masked", buf, 4096, 4096, 0, 255, 2, true);
     RunStrided("strided 4101 / 4097 masked (init)", buf, 4101, 4097, 0x12345678u, 255, 2, true);

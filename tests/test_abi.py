@@ -127,7 +127,10 @@ def test_lane_packed_kernels_emulated(tmp_path):
     atomics in host memory, DMA copies range-checked), run over every span
     shape (short spans packed per iteration, table blocks, long spans shared
     through the workgroup queue, empties, inits, masks), verify with
-    corruptions, and strided blocks -- bit-exact with a byte-serial CRC."""
+    corruptions, and strided blocks -- bit-exact with a byte-serial CRC.
+    The launch-level pipeline choice (run_ea for 4 KiB-class and >= 32 KiB
+    batches, run_lp otherwise) is checked per shape, and a second run forces
+    run_ea on every shape."""
     clang = "/opt/rocm/lib/llvm/bin/clang++"
     if not os.path.exists(clang):
         pytest.skip("ROCm clang++ not present")
@@ -136,6 +139,13 @@ def test_lane_packed_kernels_emulated(tmp_path):
                     "-I", os.path.join(REPO, "wipdb_amd", "csrc"), "-I", os.path.join(REPO, "tests", "cpp"),
                     os.path.join(REPO, "tests", "cpp", "test_lp_emu.cc"), "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "PASS" in r.stdout
+    # the same shapes with every launch forced onto run_ea (the launch's
+    # pipeline choice only changes speed: both pipelines must be exact on
+    # every shape, whatever the sample picked)
+    r = subprocess.run([exe, "--pipe=ea", "one", "17", "tiny", "short", "bucket", "near", "small pieces",
+                        "long", "zipf", "verify", "strided"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "PASS" in r.stdout
 

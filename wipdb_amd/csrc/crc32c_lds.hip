@@ -37,6 +37,7 @@
 #include <stdint.h>
 
 #include "crc32c_dev.h"
+#include "crc32c_ea.h"
 
 namespace wipdb {
 namespace lk {
@@ -991,6 +992,35 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
 }
 
 // ---------------------------------------------------------------------------
+// The pipeline of a launch.  run_lp packs short spans (3.3-3.7 TiB/s on the
+// 512 B .. 2 KiB buckets, where run_ea gives each span a whole iteration:
+// 0.75-3 TiB/s) and wins on 4-8 KiB SST-packed spans; run_ea -- round 2's
+// lean one-span-per-iteration loop -- is 2-6 % faster on aligned 4 KiB
+// blocks, table blocks (4 KiB + a front of <= 16 chunks), ReadBlock's 4 KiB
+// blocks and spans of >= 32 KiB (same-session A/Bs).
+// Every wave of every workgroup samples the same 64 spans spread over the
+// batch (one vector load per lane) and takes run_ea only when all of them
+// suit it, so a workgroup's waves always agree (the two pipelines use the
+// LDS aux column differently) and a mixed batch stays on run_lp.  The choice
+// changes speed only: both compute every span exactly.
+// ---------------------------------------------------------------------------
+template <bool kV, typename Src>
+__device__ __forceinline__ bool pick_ea(const Src& src) {
+  const uint32_t l = lane_tid() & 63u;
+  const uint64_t count = src.count;
+  const uint64_t s = (count * l) >> 6;  // (count < 2^31: no overflow)
+  uint64_t a = 0;
+  uint32_t n = 0, init = 0;
+  src.lane(s, a, n, init);
+  const Plan p = MakePlan(a, static_cast<uint32_t>(reinterpret_cast<uint64_t>(src.base) + a),
+                          src.bytes(n), kV);
+  // one segment + a front of <= 16 chunks (run_ea's batched pieces), or a
+  // span of >= 32 KiB
+  const bool ok = p.empty || (p.C >= kSegChunks && p.C <= kSegChunks + 16u) || p.C >= 8u * kSegChunks;
+  return pipeline_marker(ballot(!ok) == 0u);
+}
+
+// ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
 // Descriptor batch: out[i] = Extend(inits[i], base + offsets[i], lengths[i]);
@@ -1001,7 +1031,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u};
-  run_lp<0>(src, out, flags, image);
+  if (pick_ea<false>(src)) run_ea<0>(src, out, flags, image);
+  else run_lp<0>(src, out, flags, image);
 }
 template __global__ void crc32c_lds_spans_kernel<0>(const uint8_t*, const uint64_t*,
                                                     const uint32_t*, const uint32_t*, uint32_t*,
@@ -1015,7 +1046,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t length, uint32_t init,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
   const StridedSrc src{base, stride, length, init, count};
-  run_lp<0>(src, out, flags & kFlagMask, image);
+  if (pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
+  else run_lp<0>(src, out, flags & kFlagMask, image);
 }
 
 // Read-side verify (ReadBlock, kv/src/table/format.cc:91-99): block i =
@@ -1026,7 +1058,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
     const uint8_t* __restrict__ image) {
   const DescSrc<false> src{base, offsets, lengths, nullptr, count, 1u};
-  run_lp<1>(src, status, 0u, image);
+  if (pick_ea<true>(src)) run_ea<1>(src, status, 0u, image);
+  else run_lp<1>(src, status, 0u, image);
 }
 
 }  // namespace lk

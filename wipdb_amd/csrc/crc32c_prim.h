@@ -62,6 +62,9 @@ __device__ __forceinline__ uint32_t vzero() { return __builtin_amdgcn_mbcnt_lo(0
 // A queue record's marker as read (the host emulation can hide one to force
 // the timeout path; here the identity).
 __device__ __forceinline__ uint32_t queue_marker(uint32_t v, uint32_t) { return v; }
+// the pipeline a launch's waves chose (run_ea if true): identity here; the
+// host emulation records it and can force either one
+__device__ __forceinline__ bool pipeline_marker(bool ea) { return ea; }
 
 // ---- lanes ----
 __device__ __forceinline__ uint32_t lane_tid() { return threadIdx.x; }
