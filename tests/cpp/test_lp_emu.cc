@@ -293,6 +293,7 @@ int main(int argc, char** argv) {
     SetRange(buf);
     emu::g_spin = 64;
     emu::g_hide_marker = 0;
+    emu::g_pipes = 0;
     const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
     emu::launch(1, [&] {
       crc32c_lds_spans_kernel<0>(buf.data(), o.data(), l.data(), nullptr, got.data(), l.size(), 0u,
