@@ -297,7 +297,38 @@ __device__ __forceinline__ uint32_t le32_at(const u32x4& lo, const u32x4& hi, ui
 // ((u / 16) * grid + wg) * 16 + u % 16 -- blocks of 16 spans round robin
 // over the grid, so the chip reads one compact window of the batch at a
 // time, and within a workgroup whichever wave is free takes the next span.
+// The spans past the last whole round (count mod 16 grid) go round robin one
+// at a time (unit u >= full: span u * grid + wg), so no workgroup holds more
+// than one span beyond another's: blocks of 16 left up to 16 long spans on
+// one workgroup while others had none (config 3's 32 / 64 KiB buckets:
+// 15.04 / 7.52 blocks per workgroup, the launch paced by 16 / 8).
 // ---------------------------------------------------------------------------
+struct WgUnits {
+  uint32_t full;   // units in whole rounds (a multiple of 16)
+  uint32_t count;  // the workgroup's units
+};
+__device__ __forceinline__ WgUnits wg_units(uint64_t count) {
+  const uint64_t G = group_count(), g = group_id();
+  const uint64_t full = count / (16u * G) * 16u;
+  const uint64_t rest = count - full * G;  // < 16 G
+  WgUnits u;
+  u.full = static_cast<uint32_t>(full);
+  u.count = static_cast<uint32_t>(full + (rest > g ? (rest - g - 1u) / G + 1u : 0u));
+  return u;
+}
+__device__ __forceinline__ uint64_t unit_span(uint32_t u, uint32_t full) {
+  const uint64_t G = group_count(), g = group_id();
+  return u < full ? (static_cast<uint64_t>(u >> 4) * G + g) * 16u + (u & 15u)
+                  : static_cast<uint64_t>(u) * G + g;
+}
+// One unit (run_ea): its span (>= count once the workgroup's units are out).
+__device__ __forceinline__ uint64_t grab_unit(uint32_t l, uint32_t full) {
+  uint32_t u = 0;
+  if (l == 0u) u = lds_add(MiscAddr(kMiscUnit), 1u);
+  return unit_span(uni(u), full);
+}
+// N units at once (the size-class list kernels: N consecutive spans of one
+// 16-span block, whole rounds only).
 template <uint32_t N>
 __device__ __forceinline__ uint64_t grab_units(uint32_t l) {
   uint32_t u = 0;

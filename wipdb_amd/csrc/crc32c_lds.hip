@@ -245,7 +245,8 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   const uint32_t l = lane_tid() & 63u;
   const uint32_t w = uni(lane_tid() >> 6);
   const uint64_t count = src.count;
-  if (static_cast<uint64_t>(group_id()) * 16u >= count) return;  // no block of work
+  const WgUnits units = wg_units(count);
+  if (units.count == 0u) return;  // no unit of work
   load_image(image, w, l);
   const Lane lk = make_lane<1>(l);
   Pipe pp;
@@ -301,19 +302,12 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   uint32_t carry = 0, carry_tw = 0;   // the split piece's register over its first lanes, tail word
   uint32_t chain = 0;
 
-  // The workgroup's units: unit u is span ((u / 16) * grid + wg) * 16 +
-  // u % 16 -- blocks of 16 spans round robin over the grid, so the chip
-  // reads one compact window of the batch at a time; ug = its unit count.
-  auto span_of = [&](uint32_t un) -> uint64_t {
-    return (static_cast<uint64_t>(un >> 4) * group_count() + group_id()) * 16u + (un & 15u);
-  };
-  uint32_t ug = 0;
-  {
-    const uint64_t nblk = (count + 15u) >> 4, g = group_id(), G = group_count();
-    const uint64_t nbg = (nblk - 1u - g) / G + 1u;  // (g < nblk: checked above)
-    const bool partial_last = (nblk - 1u) % G == g;
-    ug = static_cast<uint32_t>(nbg * 16u - (partial_last ? nblk * 16u - count : 0u));
-  }
+  // The workgroup's units (crc32c_dev.h wg_units): blocks of 16 spans round
+  // robin over the grid, so the chip reads one compact window of the batch
+  // at a time, then the spans past the last whole round one at a time; ug =
+  // its unit count.
+  auto span_of = [&](uint32_t un) -> uint64_t { return unit_span(un, units.full); };
+  const uint32_t ug = units.count;
   // A desk: one unit-counter add, the descriptors loaded (lanes 0 .. size -
   // 1; waited for at first use).  kDesk units while the workgroup has
   // plenty left, then 16 and 8 (the waves' last desks end close together).
