@@ -334,6 +334,9 @@ int main(int argc, char** argv) {
     auto l2 = lens_of(1000, 4096, 4225);
     g_want_pipe = 1;
     RunVerify("verify table blocks", buf, Packed(l2, 0, 4), l2, 3);
+    // long blocks (run_ea), good and corrupted
+    auto l3 = lens_of(150, 32768, 120000);
+    RunVerify("verify long 32..120 KiB", buf, Packed(l3, 6, 3), l3, 2);
     g_want_pipe = 0;
   }
   if (Want(argc, argv, "strided")) {
