@@ -24,8 +24,14 @@ The line says so ("precondition").
 
 Also printed in the same JSON line:
   roofline      the CRC kernel's average launch time from HIP events on the
-                launch stream; achieved = algorithmic bytes per launch
-                (4096 + 4 per block) / that time, vs the 8 TB/s HBM peak;
+                launch stream -- by default one event pair around the K
+                timed launches (time / K: the ~1.5 us dispatch gaps count
+                against the kernel); --events step puts a pair around every
+                launch instead (per-launch times and their minimum, but
+                ~5 us of event packets between launches inside the timed
+                region: profiles/r04x_events.log); achieved = algorithmic
+                bytes per launch (4096 + 4 per block) / that time, vs the
+                8 TB/s HBM peak;
                 traffic = PMC HBM bytes per launch from the committed rocprof
                 profile of this config (profiles/traffic.json), or null.
   cpu_baseline  the reference kv::crc32c (oracle/_ref, compiled from the
@@ -65,6 +71,9 @@ def parse():
     p.add_argument("--blocks", type=int, default=0,
                    help="blocks per GPU (default: 1 M at N = 1, 8 M per rank at N > 1)")
     p.add_argument("--mode", choices=["spans", "strided"], default="spans")
+    p.add_argument("--events", choices=["step", "bracket"], default="bracket",
+                   help="HIP events around every timed launch (per-launch kernel times) or "
+                        "only around the timed region (no event between launches)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=5.0,
                    help="minimum time of the 1-thread reference baseline (whole passes)")
@@ -236,19 +245,26 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    nev = a.steps if a.events == "step" else 1
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(a.steps)]
+          for _ in range(nev)]
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
-        step()
-        e.record(stream)
+    if a.events == "step":
+        for s, e in ev:
+            s.record(stream)
+            step()
+            e.record(stream)
+    else:
+        ev[0][0].record(stream)
+        for _ in range(a.steps):
+            step()
+        ev[0][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = [s.elapsed_time(e) for s, e in ev]
+    kern_ms = [s.elapsed_time(e) * nev / a.steps for s, e in ev]
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
     elapsed_max = max_over_ranks(elapsed, dev)
@@ -317,7 +333,9 @@ def main():
                 "traffic": committed_traffic(a.mode, nblk),
                 "kernel": KERNEL[a.mode],
                 "kernel_avg_ms": round(kern_avg_ms, 4),
-                "kernel_min_ms": round(min(kern_ms), 4),
+                "kernel_min_ms": round(min(kern_ms), 4) if a.events == "step" else None,
+                "kernel_timing": ("HIP events around each timed launch" if a.events == "step" else
+                                  "HIP events around the timed launches / K"),
                 "algorithmic_bytes_per_launch": nblk * ALGO_BYTES_PER_BLOCK,
             },
             "precondition": pre,
