@@ -457,6 +457,26 @@ def test_batch_counts_work_sharing(engine, oracle, count):
     np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
 
 
+@pytest.mark.parametrize("kind", ["short", "long"])
+@pytest.mark.parametrize("count", [4095, 4096, 4097, 4351, 4352, 4353, 8448 + 77])
+def test_last_round_spans_one_at_a_time(engine, oracle, kind, count):
+    """The spans past the last whole round of 16-span blocks (count mod
+    16 x 256 on 256 CUs) are dealt one at a time, span u * grid + workgroup
+    (crc32c_dev.h wg_units / unit_span): counts just under, at and past whole
+    rounds, on both pipelines of a launch -- short spans (run_lp) and spans of
+    >= 32 KiB (run_ea) -- every span computed once, into its own slot."""
+    rng = np.random.default_rng(count + (0 if kind == "short" else 1))
+    buf = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
+    if kind == "short":
+        lens = rng.integers(0, 9000, count).astype(np.uint32)
+    else:
+        lens = rng.integers(32768, 36865, count).astype(np.uint32)
+    offs = rng.integers(0, buf.size - 36865, count).astype(np.uint64)
+    inits = rng.integers(0, 2**32, size=count, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(buf, offs, lens, inits)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
+
+
 @pytest.mark.parametrize("count", [262144, 262145, 262144 + 31, 262144 + 33, 300001, 1 << 20])
 def test_pool_counts(engine, oracle, count):
     """Batches past the workgroups' static share (32 rounds x 256 CUs x 32
