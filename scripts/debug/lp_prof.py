@@ -35,6 +35,11 @@ def shape(name):
         ln = rng.integers(4097, 4226, n).astype(np.int64)
         offs = np.concatenate([[0], np.cumsum(ln + 4)[:-1]])
         return offs.astype(np.int64), ln.astype(np.int32), int(offs[-1] + ln[-1] + 64)
+    if name == "zipf":  # config 3's mix: Zipf(0.99) over 512 B .. 64 KiB (+0..L/8), SST-packed
+        sys.path.insert(0, os.path.join(REPO, "scripts"))
+        from bench_extra import BUCKETS, zipf_spans
+        offs, lens, _ = zipf_spans(np.random.default_rng(42), 2 << 30, BUCKETS)
+        return offs.astype(np.int64), lens.astype(np.int32), 2 << 30
     if name.startswith("bucket"):  # bucketN: SST-packed N-byte spans + 5-byte trailers
         b = int(name[6:])
         n = (4 << 30) // (b + 5)
