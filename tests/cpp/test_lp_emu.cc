@@ -267,6 +267,11 @@ int main(int argc, char** argv) {
     RunSpans("long 32..200 KiB (inits)", buf, Packed(l2, 5, 3), l2, &in2, true, 2);
     g_want_pipe = 0;
   }
+  // the shapes of run_lp's long-span queue: its spans are all >= 16 KiB,
+  // which the launch-level choice gives run_ea, so run_lp is forced (unless
+  // the command line forces a pipeline)
+  const bool force_lp = emu::g_force_pipe.load() < 0;
+  if (force_lp) emu::g_force_pipe = 0;
   if (Want(argc, argv, "shared long")) {  // one wave's desks of long spans, the others idle: shared
     auto l = lens_of(16, 20000, 70000);
     auto in = inits_of(l.size());
@@ -310,6 +315,7 @@ int main(int argc, char** argv) {
            l.size(), ok ? "ok" : "FAIL", fb, lost);
     if (!ok) ++g_fail;
   }
+  if (force_lp) emu::g_force_pipe = -1;
   if (Want(argc, argv, "zipf mix")) {
     const uint32_t B[] = {512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
     std::vector<uint32_t> l;

@@ -6,7 +6,7 @@
 // (crc32c_list.hip: HCRC_SPLIT_SMALL's long class, HCRC_SPLIT_LONG's parts)
 // and by the spans / verify / strided kernels for batches whose sampled spans
 // all suit it (crc32c_lds.hip pick_pipeline: aligned 4 KiB blocks, table
-// blocks, ReadBlock's 4 KiB blocks, spans of >= 32 KiB).  DESIGN.md section 4.
+// blocks, ReadBlock's 4 KiB blocks, spans of >= 16 KiB).  DESIGN.md section 4.
 //
 // Reference function: kv::crc32c::Extend (kv/src/util/crc32c.h:24,
 // kv/src/util/crc32c.cc:1225-1227) applied per block span, as

@@ -991,7 +991,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
 // 0.75-3 TiB/s) and wins on 4-8 KiB SST-packed spans; run_ea -- round 2's
 // lean one-span-per-iteration loop -- is 2-6 % faster on aligned 4 KiB
 // blocks, table blocks (4 KiB + a front of <= 16 chunks), ReadBlock's 4 KiB
-// blocks and spans of >= 32 KiB (same-session A/Bs).
+// blocks and spans of >= 16 KiB (same-session A/Bs).
 // Every wave of every workgroup samples the same 64 spans spread over the
 // batch (one vector load per lane) and takes run_ea only when all of them
 // suit it, so a workgroup's waves always agree (the two pipelines use the
@@ -1009,8 +1009,8 @@ __device__ __forceinline__ bool pick_ea(const Src& src) {
   const Plan p = MakePlan(a, static_cast<uint32_t>(reinterpret_cast<uint64_t>(src.base) + a),
                           src.bytes(n), kV);
   // one segment + a front of <= 16 chunks (run_ea's batched pieces), or a
-  // span of >= 32 KiB
-  const bool ok = p.empty || (p.C >= kSegChunks && p.C <= kSegChunks + 16u) || p.C >= 8u * kSegChunks;
+  // span of >= 16 KiB
+  const bool ok = p.empty || (p.C >= kSegChunks && p.C <= kSegChunks + 16u) || p.C >= 4u * kSegChunks;
   return pipeline_marker(ballot(!ok) == 0u);
 }
 
