@@ -74,6 +74,15 @@ def main():
             ms = e0.elapsed_time(e1) / reps
             assert fn(host.ctypes.data, host.nbytes, 1) == 0
             p = host.reshape(4096, NPROF).astype(np.float64) / reps
+            # wave lifetimes per workgroup (slot = workgroup * 16 + wave):
+            # the spread across workgroups vs within them
+            lifeg = p[:, 7].reshape(256, 16)
+            wg = lifeg[(lifeg > 0).all(axis=1)]
+            if len(wg):
+                wmax, wmean = wg.max(axis=1), wg.mean(axis=1)
+                print(f"  workgroups: last wave at {wmax.min():.0f} .. {wmax.max():.0f} cycles "
+                      f"(mean {wmax.mean():.0f}, max/mean {wmax.max() / wmax.mean():.3f}); "
+                      f"within a workgroup mean wave / last wave {np.mean(wmean / wmax):.3f}")
             live = p[:, 7] > 0
             p = p[live]
             it = p[:, 4] + p[:, 5] + p[:, 6]
