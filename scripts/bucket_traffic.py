@@ -7,6 +7,7 @@ hcrc_batch_async entry point (no flags), in bucket order, so a rocprofv3
 
   python scripts/bucket_traffic.py run            # the launches (under rocprofv3)
   python scripts/bucket_traffic.py summarize FETCH_DIR WRITE_DIR > out.json
+  python scripts/bucket_traffic.py summarize_sq SQ_DIR > out.json  # SQ_* pass
 
 Algorithmic bytes per launch: the spans' bytes read + 4 bytes
 written per span; the descriptor columns (8 + 4 bytes per span) are listed
@@ -58,6 +59,41 @@ def run():
     print(json.dumps(meta))
 
 
+def counters_of(d):
+    names = set()
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            names.update(r["Counter_Name"] for r in csv.DictReader(f) if KERNEL in r["Kernel_Name"])
+    return sorted(names)
+
+
+def summarize_sq(sdir):
+    """Per-bucket SQ counters per span and per wave (mean of the launches)."""
+    with open(os.path.join(REPO, "gpurun_out", "bucket_traffic_meta.json")) as f:
+        meta = json.load(f)
+    need = LAUNCHES * len(meta)
+    cols = {}
+    for c in counters_of(sdir):
+        v = per_dispatch(sdir, c)
+        if len(v) != need:
+            sys.exit(f"{c}: expected {need} dispatches, got {len(v)}")
+        cols[c] = v
+    out = []
+    for k, m in enumerate(meta):
+        row = dict(m)
+        for c, v in cols.items():
+            row[c] = round(sum(v[k * LAUNCHES:(k + 1) * LAUNCHES]) / LAUNCHES)
+        if "SQ_WAVE_CYCLES" in row and row.get("SQ_WAVES"):
+            row["wave_cycles_per_wave"] = round(row["SQ_WAVE_CYCLES"] / row["SQ_WAVES"])
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAIT_INST_ANY"):
+            if c in row:
+                row[c + "_per_span"] = round(row[c] / m["spans"], 2)
+        out.append(row)
+    print(json.dumps({"source": "rocprofv3 --pmc SQ_* (one pass), "
+                                f"mean of {LAUNCHES} launches per bucket, default entry point",
+                      "buckets": out}, indent=1))
+
+
 def per_dispatch(d, counter):
     rows = []
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -101,5 +137,7 @@ if __name__ == "__main__":
         run()
     elif sys.argv[1:2] == ["summarize"]:
         summarize(sys.argv[2], sys.argv[3])
+    elif sys.argv[1:2] == ["summarize_sq"]:
+        summarize_sq(sys.argv[2])
     else:
         sys.exit(__doc__)

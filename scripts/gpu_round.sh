@@ -41,6 +41,10 @@ for s in $STEPS; do
     bucket_pmc) run bucket_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${P}_bfetch -o run --output-format csv -- python3 scripts/bucket_traffic.py run &&
                 run bucket_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${P}_bwrite -o run --output-format csv -- python3 scripts/bucket_traffic.py run &&
                 python3 scripts/bucket_traffic.py summarize gpurun_out/${P}_bfetch gpurun_out/${P}_bwrite > gpurun_out/${P}_bucket_traffic.json; tail -40 gpurun_out/${P}_bucket_traffic.json ;;
+    bucket_sq) run bucket_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_SMEM -d gpurun_out/${P}_bsq -o run --output-format csv -- python3 scripts/bucket_traffic.py run &&
+                python3 scripts/bucket_traffic.py summarize_sq gpurun_out/${P}_bsq > gpurun_out/${P}_bucket_sq.json; tail -30 gpurun_out/${P}_bucket_sq.json ;;
+    shape_sq) run shape_sq 600 bash scripts/pmc_shape_ab.sh tblocks tree &&
+              run shape_sq_v 600 env KERNEL=verify bash scripts/pmc_shape_ab.sh vtblocks tree ;;
     pmc_sq) run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM -d gpurun_out/${P}_pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s" ;;
   esac
