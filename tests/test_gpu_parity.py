@@ -477,6 +477,88 @@ def test_last_round_spans_one_at_a_time(engine, oracle, kind, count):
     np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits), want)
 
 
+def _ea_sample(count):
+    """The 64 spans a launch samples for its pipeline choice
+    (crc32c_lds.hip pick_ea: span count * lane >> 6 of each lane)."""
+    return np.unique((np.arange(64, dtype=np.uint64) * np.uint64(count)) >> np.uint64(6))
+
+
+@pytest.mark.parametrize("kind", ["4k", "long"])
+def test_ea_launch_with_unsampled_odd_spans(engine, oracle, kind):
+    """A launch whose 64 sampled spans all suit run_ea (4 KiB-class blocks,
+    or spans of >= 16 KiB) takes run_ea for the whole batch; every other span
+    here is an arbitrary shape (empty, a few bytes, short, 4 KiB + piece,
+    long), at random offsets and with inits: run_ea must compute them all
+    exactly, plain and masked."""
+    rng = np.random.default_rng(31 if kind == "4k" else 32)
+    count = 6001
+    buf = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
+    lens = rng.choice(np.array([0, 1, 3, 15, 16, 17, 100, 511, 4095, 4097, 4224, 9000, 20000],
+                               np.uint32), count)
+    offs = rng.integers(0, buf.size - 40000, count).astype(np.uint64)
+    s = _ea_sample(count)
+    if kind == "4k":
+        lens[s] = 4096
+        offs[s] = rng.integers(0, buf.size // 4096 - 16, s.size).astype(np.uint64) * 4096
+    else:
+        lens[s] = rng.integers(16384, 40000, s.size).astype(np.uint32)
+    inits = rng.integers(0, 2**32, size=count, dtype=np.uint64).astype(np.uint32)
+    for mask in (False, True):
+        want = oracle.batch(buf, offs, lens, inits, mask=mask)
+        np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits, mask=mask), want)
+
+
+def test_ea_verify_launch_with_unsampled_odd_blocks(engine, oracle):
+    """ReadBlock verify (kv/src/table/format.cc:91-99) where the sampled
+    blocks are table blocks (run_ea) and the rest are blocks of 0..20000
+    content bytes, SST-packed; a quarter corrupted, in contents, type byte or
+    trailer."""
+    import torch
+    rng = np.random.default_rng(33)
+    count = 3001
+    s = set(_ea_sample(count).tolist())
+    buf = np.zeros(48 << 20, np.uint8)
+    offs, lens, cur = [], [], 0
+    for i in range(count):
+        n = int(rng.integers(4096, 4200)) if i in s else int(rng.choice([0, 1, 7, 300, 4091, 4300, 20000]))
+        buf[cur:cur + n] = rng.integers(0, 256, n, dtype=np.uint8)
+        buf[cur + n] = i & 1
+        offs.append(cur)
+        lens.append(n)
+        cur += n + 5 + int(rng.integers(0, 3))
+    offs, lens = np.array(offs, np.uint64), np.array(lens, np.uint32)
+    crcs = oracle.batch(buf, offs, lens + 1)
+    for o, n, c in zip(offs, lens, crcs):
+        m = int(oracle.lib.oracle_mask(int(c)))
+        buf[int(o) + int(n) + 1:int(o) + int(n) + 5] = np.frombuffer(m.to_bytes(4, "little"), np.uint8)
+    bad = rng.choice(np.array(sorted(set(range(count)) - s)), count // 4, replace=False)
+    for i, b in enumerate(bad):
+        o, n = int(offs[b]), int(lens[b])
+        where = [o + (int(rng.integers(0, n)) if n else n), o + n, o + n + 1 + int(rng.integers(0, 4))][i % 3]
+        buf[where] ^= 0x21
+    expect = np.ones(count, np.uint8)
+    expect[bad] = 0
+    st = engine.verify_device(_t(buf), _t(offs), _t(lens))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st.cpu().numpy(), expect)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_batches_every_shape(engine, oracle, seed):
+    """Seeded batches of log-uniform lengths (0 .. 256 KiB, empty spans
+    included) at random, overlapping offsets, with inits, plain and masked:
+    whichever pipeline the launch picks, every CRC equals the oracle's."""
+    rng = np.random.default_rng(1000 + seed)
+    count = int(rng.integers(1, 5000))
+    buf = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
+    lens = np.exp(rng.uniform(0, np.log(256 << 10), count)).astype(np.uint32) - 1
+    offs = rng.integers(0, buf.size - (256 << 10), count).astype(np.uint64)
+    inits = rng.integers(0, 2**32, size=count, dtype=np.uint64).astype(np.uint32)
+    mask = bool(seed & 1)
+    want = oracle.batch(buf, offs, lens, inits, mask=mask)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, inits, mask=mask), want)
+
+
 @pytest.mark.parametrize("count", [262144, 262145, 262144 + 31, 262144 + 33, 300001, 1 << 20])
 def test_pool_counts(engine, oracle, count):
     """Batches past the workgroups' static share (32 rounds x 256 CUs x 32
