@@ -98,6 +98,16 @@ extern "C" {
  * HCRC_SPLIT_SMALL.  A device batch of at most 16 spans (without
  * HCRC_SPLIT_SMALL) takes it by itself: there one long span is the job. */
 #define HCRC_SPLIT_LONG 0x8
+/* Byte-balanced workgroups (device descriptor batches, hcrc_batch_async /
+ * hcrc_batch with HCRC_DEVICE_PTRS): two small passes over the length
+ * column cut the batch into one contiguous range per workgroup of equal
+ * weight (bytes + 64 per span), instead of dealing every workgroup the same
+ * NUMBER of spans.  For large batches of mixed sizes (config 3's Zipf mix:
+ * the default deal leaves the busiest of 256 workgroups ~1.17x the mean);
+ * same results, two extra launches and (G + 1) * 4 + 8 * n / 1024 bytes of
+ * stream-ordered scratch.  Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG
+ * and for batches of fewer than 64 spans per workgroup. */
+#define HCRC_BALANCE 0x10
 
 typedef struct hcrc_ctx hcrc_ctx;
 

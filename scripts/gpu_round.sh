@@ -17,6 +17,10 @@ run() {  # name timeout cmd...
   echo "=== $name rc=$rc ($(( $(date +%s) - t0 )) s)" | tee -a gpurun_out/steps.log
   grep -v "amdgpu.ids" "gpurun_out/${P}_$name.log" | tail -${TAILN:-6}
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  # a Python exception from a GPU fault exits 1: nothing more on the GPU
+  if grep -q -E "illegal memory access|hipErrorIllegalAddress|Memory access fault" "gpurun_out/${P}_$name.log"; then
+    echo "ABORT after $name (GPU fault)"; exit 3
+  fi
   return 0
 }
 for s in $STEPS; do
@@ -33,6 +37,8 @@ for s in $STEPS; do
     long) run long 300 python scripts/long_span_probe.py ;;
     lpprof) run lpprof 300 python -u scripts/debug/lp_prof.py ${LPPROF_SHAPES:-headline tblocks bucket512 bucket1024 bucket2048 bucket65536} ;;
     autosplit) run autosplit 500 python -u scripts/autosplit_ab.py ;;
+    balance) run balance 500 python -u scripts/balance_ab.py ${BAL_ROUNDS:-3} ;;
+    balance_prof) run balance_prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_balprof -o run --output-format csv -- python scripts/balance_ab.py 1 ;;
     cfg4) run cfg4 400 python bench.py --blocks 8388608 --steps 10 --warmup 5 ;;
     ab) run ab 900 bash scripts/gpu_abn.sh ${AB_ROUNDS:-2} ${AB_WHAT:-mixed,tblocks,vtblocks,verify} tree ${AB_LIBS:-build/ab/lib_r02.so} ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;

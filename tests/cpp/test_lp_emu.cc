@@ -79,11 +79,37 @@ void Report(const char* name, const std::vector<uint32_t>& got, const std::vecto
   if (fail) ++g_fail;
 }
 
+// HCRC_BALANCE's workgroup ranges, restated on the host
+// (util::balance_bounds_kernel): bounds[g] = #{i : excl(i) < g T / G},
+// weight = length + 64.  g_balance: RunSpans passes them to the kernel.
+bool g_balance = false;
+std::vector<uint32_t> BalanceBounds(const std::vector<uint32_t>& lens, uint32_t G) {
+  uint64_t T = 0;
+  for (uint32_t n : lens) T += n + 64u;
+  std::vector<uint32_t> b(G + 1, 0);
+  b[G] = static_cast<uint32_t>(lens.size());
+  for (uint32_t g = 1; g < G; ++g) {
+    const uint64_t target = (T / G) * g + (T % G) * g / G;
+    uint64_t e = 0;
+    uint32_t c = 0;
+    for (uint32_t n : lens) {
+      if (e >= target) break;
+      ++c;
+      e += n + 64u;
+    }
+    b[g] = c;
+  }
+  return b;
+}
+
 // CRC batch through crc32c_lds_spans_kernel
 void RunSpans(const char* name, std::vector<uint8_t>& buf, const std::vector<uint64_t>& offs,
               const std::vector<uint32_t>& lens, const std::vector<uint32_t>* inits, bool mask,
               uint32_t cus) {
   const size_t n = offs.size();
+  const std::vector<uint32_t> bounds =
+      g_balance ? BalanceBounds(lens, Grid(n, cus)) : std::vector<uint32_t>();
+  const uint32_t* bd = g_balance ? bounds.data() : nullptr;
   std::vector<uint32_t> want(n), got(n, 0x5A5A5A5Au);
   for (size_t i = 0; i < n; ++i) {
     const uint32_t c = Extend(inits ? (*inits)[i] : 0u, buf.data() + offs[i], lens[i]);
@@ -94,10 +120,10 @@ void RunSpans(const char* name, std::vector<uint8_t>& buf, const std::vector<uin
   emu::launch(Grid(n, cus), [&] {
     if (inits)
       crc32c_lds_spans_kernel<1>(buf.data(), offs.data(), lens.data(), inits->data(), got.data(), n,
-                                 mask ? kFlagMask : 0u, img);
+                                 mask ? kFlagMask : 0u, img, bd);
     else
       crc32c_lds_spans_kernel<0>(buf.data(), offs.data(), lens.data(), nullptr, got.data(), n,
-                                 mask ? kFlagMask : 0u, img);
+                                 mask ? kFlagMask : 0u, img, bd);
   });
   Report(name, got, want, offs, lens);
 }
@@ -302,7 +328,7 @@ int main(int argc, char** argv) {
     const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
     emu::launch(1, [&] {
       crc32c_lds_spans_kernel<0>(buf.data(), o.data(), l.data(), nullptr, got.data(), l.size(), 0u,
-                                 img);
+                                 img, nullptr);
     });
     emu::g_spin = 1u << 22;
     emu::g_hide_marker = ~0u;
@@ -332,7 +358,20 @@ int main(int argc, char** argv) {
     }
     g_want_pipe = 2;
     RunSpans("zipf mix", buf, Packed(l, 3, 5), l, nullptr, false, 4);
+    // HCRC_BALANCE: contiguous byte-balanced workgroup ranges, both pipelines
+    g_balance = true;
+    RunSpans("zipf mix balanced", buf, Packed(l, 3, 5), l, nullptr, false, 4);
     g_want_pipe = 0;
+    {
+      std::vector<uint32_t> in(l.size());
+      for (auto& x : in) x = static_cast<uint32_t>(rng());
+      RunSpans("zipf mix balanced (inits, mask)", buf, Packed(l, 6, 5), l, &in, true, 3);
+    }
+    auto l4 = lens_of(1200, 4096, 4096);
+    std::vector<uint64_t> o4(l4.size());
+    for (size_t i = 0; i < o4.size(); ++i) o4[i] = i * 4096;
+    RunSpans("aligned 4 KiB balanced", buf, o4, l4, nullptr, false, 3);
+    g_balance = false;
   }
   if (Want(argc, argv, "verify")) {
     auto l = lens_of(1500, 1, 5000);

@@ -38,11 +38,11 @@ def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
 
-def _run_device(engine, buf, offs, lens, inits=None, mask=False, split=False):
+def _run_device(engine, buf, offs, lens, inits=None, mask=False, split=False, balance=False):
     out = engine.batch_device(_t(buf), _t(np.asarray(offs, np.uint64)),
                               _t(np.asarray(lens, np.uint32)),
                               None if inits is None else _t(np.asarray(inits, np.uint32)),
-                              mask_output=mask, split_small=split)
+                              mask_output=mask, split_small=split, balance=balance)
     return _u32(out)
 
 
@@ -622,6 +622,30 @@ def test_zipf_mixed_sst_packing(engine, oracle):
     want = oracle.batch(buf, offs, lens)
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, split=True), want)
+
+
+@pytest.mark.parametrize("n,lo,hi", [(40000, 0, 3000), (70001, 1, 600), (20011, 4096, 4225),
+                                      (17000, 1, 70000)])
+def test_balanced_workgroups(engine, oracle, n, lo, hi):
+    """HCRC_BALANCE (util::balance_sums/bounds_kernel + contiguous workgroup
+    ranges in the spans kernel): every span exactly once, bit-exact with the
+    oracle -- log-uniform sizes (a few huge spans skew the cut), empty spans,
+    inits and masked output, batches at and just past 64 spans per workgroup,
+    and table-block shapes (run_ea)."""
+    rng = np.random.default_rng(n)
+    lens = np.exp(rng.uniform(np.log(max(lo, 1)), np.log(hi + 1), n)).astype(np.uint32)
+    lens[rng.random(n) < 0.02] = 0 if lo == 0 else lo
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens.astype(np.uint64) + 3)[:-1]
+    buf = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(buf, offs, lens, inits)
+    got = _run_device(engine, buf, offs, lens, inits, balance=True)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(_run_device(engine, buf, offs, lens, balance=True),
+                                  oracle.batch(buf, offs, lens))
+    m = _run_device(engine, buf, offs, lens, inits, mask=True, balance=True)
+    np.testing.assert_array_equal(m, oracle.batch(buf, offs, lens, inits, mask=True))
 
 
 def test_full_size_4k_blocks(engine, oracle, reference):

@@ -19,8 +19,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HCRC_SPLIT_LONG, HCRC_SPLIT_SMALL,
-                   HcrcError, check)
+from ._lib import (HCRC_BALANCE, HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HCRC_SPLIT_LONG,
+                   HCRC_SPLIT_SMALL, HcrcError, check)
 
 MASK_DELTA = 0xA282EAD8
 
@@ -193,12 +193,14 @@ class Engine:
 
     def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
                      mask_output: bool = False, stream=None, split_small: bool = False,
-                     check_bounds: bool = False, split_long: bool = False):
+                     check_bounds: bool = False, split_long: bool = False,
+                     balance: bool = False):
         """Asynchronous batch on device tensors; returns the uint32 out tensor
         (int32 storage).  Enqueued on ``stream`` (default: torch's current).
         ``split_small``: HCRC_SPLIT_SMALL (the size classes); ``split_long``:
         HCRC_SPLIT_LONG (spans of >= 128 KiB in 16 KiB parts on many waves;
-        batches of at most 16 spans take it by themselves).  Offsets are
+        batches of at most 16 spans take it by themselves); ``balance``:
+        HCRC_BALANCE (byte-balanced workgroup ranges for mixed sizes).  Offsets are
         int64, lengths / inits / out 32-bit, all contiguous on this engine's
         device; ``check_bounds`` also checks every span against base (a
         device kernel and a sync, hcrc_check_spans)."""
@@ -212,6 +214,8 @@ class Engine:
             flags |= HCRC_SPLIT_SMALL
         if split_long:
             flags |= HCRC_SPLIT_LONG
+        if balance:
+            flags |= HCRC_BALANCE
         check(self._lib.hcrc_batch_async(self._ctx, _ptr(base_t), _ptr(offsets_t), _ptr(lengths_t),
                                          _ptr(inits_t), _ptr(out_t), n, flags,
                                          self._stream_of(stream)), "hcrc_batch_async")

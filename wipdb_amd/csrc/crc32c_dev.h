@@ -221,6 +221,7 @@ struct DescSrc {
   const uint32_t* init;
   uint64_t count;
   uint32_t extra;  // verify: +1 type byte
+  const uint32_t* bounds;  // HCRC_BALANCE: workgroup ranges (else nullptr)
   __device__ __forceinline__ SpanD get(uint64_t s) const {
     return SpanD{off[s], len[s] + extra, kInit ? init[s] : 0u, static_cast<uint32_t>(s)};
   }
@@ -303,29 +304,47 @@ __device__ __forceinline__ uint32_t le32_at(const u32x4& lo, const u32x4& hi, ui
 // one workgroup while others had none (config 3's 32 / 64 KiB buckets:
 // 15.04 / 7.52 blocks per workgroup, the launch paced by 16 / 8).
 // ---------------------------------------------------------------------------
+//
+// HCRC_BALANCE: bounds (device, G + 1 entries, util::balance_bounds_kernel)
+// give the workgroup the contiguous spans [bounds[g], bounds[g + 1]) instead,
+// cut by weight, not count (lo = its first span; full = kBalanced).
+constexpr uint32_t kBalanced = ~0u;
+template <typename Src>
+__device__ __forceinline__ const uint32_t* src_bounds(const Src&) { return nullptr; }
+template <bool kInit>
+__device__ __forceinline__ const uint32_t* src_bounds(const DescSrc<kInit>& s) { return s.bounds; }
 struct WgUnits {
-  uint32_t full;   // units in whole rounds (a multiple of 16)
+  uint32_t full;   // units in whole rounds (a multiple of 16); kBalanced: a range
   uint32_t count;  // the workgroup's units
+  uint32_t lo;     // kBalanced: the first span of the range
 };
-__device__ __forceinline__ WgUnits wg_units(uint64_t count) {
+__device__ __forceinline__ WgUnits wg_units(uint64_t count, const uint32_t* bounds) {
   const uint64_t G = group_count(), g = group_id();
+  WgUnits u;
+  if (bounds != nullptr) {
+    u.lo = bounds[g];
+    u.count = bounds[g + 1u] - u.lo;
+    u.full = kBalanced;
+    return u;
+  }
   const uint64_t full = count / (16u * G) * 16u;
   const uint64_t rest = count - full * G;  // < 16 G
-  WgUnits u;
   u.full = static_cast<uint32_t>(full);
   u.count = static_cast<uint32_t>(full + (rest > g ? (rest - g - 1u) / G + 1u : 0u));
+  u.lo = 0u;
   return u;
 }
-__device__ __forceinline__ uint64_t unit_span(uint32_t u, uint32_t full) {
+__device__ __forceinline__ uint64_t unit_span(uint32_t u, const WgUnits& w) {
   const uint64_t G = group_count(), g = group_id();
-  return u < full ? (static_cast<uint64_t>(u >> 4) * G + g) * 16u + (u & 15u)
-                  : static_cast<uint64_t>(u) * G + g;
+  if (w.full == kBalanced) return u < w.count ? static_cast<uint64_t>(w.lo) + u : ~0ull;
+  return u < w.full ? (static_cast<uint64_t>(u >> 4) * G + g) * 16u + (u & 15u)
+                    : static_cast<uint64_t>(u) * G + g;
 }
 // One unit (run_ea): its span (>= count once the workgroup's units are out).
-__device__ __forceinline__ uint64_t grab_unit(uint32_t l, uint32_t full) {
+__device__ __forceinline__ uint64_t grab_unit(uint32_t l, const WgUnits& w) {
   uint32_t u = 0;
   if (l == 0u) u = lds_add(MiscAddr(kMiscUnit), 1u);
-  return unit_span(uni(u), full);
+  return unit_span(uni(u), w);
 }
 // N units at once (the size-class list kernels: N consecutive spans of one
 // 16-span block, whole rounds only).

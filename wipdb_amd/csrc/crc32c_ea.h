@@ -78,7 +78,7 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
   const uint32_t l = lane_tid() & 63u;
   const uint32_t w = uni(lane_tid() >> 6);
   const uint64_t count = src.count;
-  const WgUnits units = wg_units(count);
+  const WgUnits units = wg_units(count, src_bounds(src));
   if (units.count == 0u) return;  // no unit of work
   load_image(image, w, l);
   const Lane lk = make_lane<1>(l);
@@ -93,7 +93,7 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
     bool valid;
   };
   auto prefetch = [&](Pref& p) {
-    const uint64_t s = grab_unit(l, units.full);
+    const uint64_t s = grab_unit(l, units);
     p.valid = s < count;
     if (p.valid) p.d = src.get(s);
   };

@@ -245,7 +245,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   const uint32_t l = lane_tid() & 63u;
   const uint32_t w = uni(lane_tid() >> 6);
   const uint64_t count = src.count;
-  const WgUnits units = wg_units(count);
+  const WgUnits units = wg_units(count, src_bounds(src));
   if (units.count == 0u) return;  // no unit of work
   load_image(image, w, l);
   const Lane lk = make_lane<1>(l);
@@ -306,7 +306,7 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // robin over the grid, so the chip reads one compact window of the batch
   // at a time, then the spans past the last whole round one at a time; ug =
   // its unit count.
-  auto span_of = [&](uint32_t un) -> uint64_t { return unit_span(un, units.full); };
+  auto span_of = [&](uint32_t un) -> uint64_t { return unit_span(un, units); };
   const uint32_t ug = units.count;
   // A desk: one unit-counter add, the descriptors loaded (lanes 0 .. size -
   // 1; waited for at first use).  kDesk units while the workgroup has
@@ -1023,17 +1023,20 @@ template <int INIT>
 __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
-    uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
-  const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u};
+    uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image,
+    const uint32_t* __restrict__ bounds) {
+  const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u, bounds};
   if (pick_ea<false>(src)) run_ea<0>(src, out, flags, image);
   else run_lp<0>(src, out, flags, image);
 }
 template __global__ void crc32c_lds_spans_kernel<0>(const uint8_t*, const uint64_t*,
                                                     const uint32_t*, const uint32_t*, uint32_t*,
-                                                    uint64_t, uint32_t, const uint8_t*);
+                                                    uint64_t, uint32_t, const uint8_t*,
+                                                    const uint32_t*);
 template __global__ void crc32c_lds_spans_kernel<1>(const uint8_t*, const uint64_t*,
                                                     const uint32_t*, const uint32_t*, uint32_t*,
-                                                    uint64_t, uint32_t, const uint8_t*);
+                                                    uint64_t, uint32_t, const uint8_t*,
+                                                    const uint32_t*);
 
 // Fixed-size blocks at a fixed stride.
 __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
@@ -1051,7 +1054,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
     const uint8_t* __restrict__ image) {
-  const DescSrc<false> src{base, offsets, lengths, nullptr, count, 1u};
+  const DescSrc<false> src{base, offsets, lengths, nullptr, count, 1u, nullptr};
   if (pick_ea<true>(src)) run_ea<1>(src, status, 0u, image);
   else run_lp<1>(src, status, 0u, image);
 }

@@ -251,5 +251,123 @@ __global__ __launch_bounds__(256) void split_combine_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Byte-balanced workgroup ranges (HCRC_BALANCE): workgroup g of the spans
+// kernel takes the contiguous spans [bounds[g], bounds[g + 1]), cut where
+// the running weight (length + 64 per span: bytes plus a per-span cost)
+// crosses g / G of the total.  The default deal (16-span blocks round robin)
+// gives every workgroup the same NUMBER of spans; on config 3's Zipf mix
+// that is max / mean 1.17 bytes per workgroup over 256 of them
+// (scripts/balance_model.py), the measured wave-lifetime spread 1.15.
+// Span i goes to the workgroup g with excl(i) in [t(g), t(g + 1)), t(g) =
+// g T / G, so bounds[g] = #{i : excl(i) < t(g)} (monotone; every span once).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), d, 64);
+    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), d, 64);
+    v += (static_cast<uint64_t>(hi) << 32) | lo;
+  }
+  return v;
+}
+// 256 threads: the exclusive prefix of v over the block, and the total.
+__device__ __forceinline__ uint64_t block_excl64(uint64_t v, uint64_t* sh, uint64_t& total) {
+  const uint32_t t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    const uint64_t u = t >= d ? sh[t - d] : 0u;
+    __syncthreads();
+    sh[t] += u;
+    __syncthreads();
+  }
+  total = sh[255];
+  const uint64_t incl = sh[t];
+  __syncthreads();
+  return incl - v;
+}
+
+// Pass 1: sums[c] = weight of chunk c (spans [c C, c C + C)).
+__global__ __launch_bounds__(256) void balance_sums_kernel(const uint32_t* __restrict__ len,
+                                                           uint64_t n, uint32_t C,
+                                                           uint64_t* __restrict__ sums) {
+  __shared__ uint64_t red[4];
+  const uint64_t lo = static_cast<uint64_t>(blockIdx.x) * C;
+  const uint64_t hi = lo + C < n ? lo + C : n;
+  uint64_t s = 0;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += 256u) s += len[i] + 64u;
+  s = wave_sum64(s);
+  if ((threadIdx.x & 63u) == 0u) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0u) sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Pass 2: one block per cut g = 1 .. G - 1 (bounds[0] = 0, bounds[G] = n
+// written by the first).  The chunk holding t(g) from the chunk sums, then
+// the spans of that chunk below t(g).
+__global__ __launch_bounds__(256) void balance_bounds_kernel(
+    const uint32_t* __restrict__ len, uint64_t n, uint32_t C, const uint64_t* __restrict__ sums,
+    uint32_t nb, uint32_t G, uint32_t* __restrict__ bounds) {
+  __shared__ uint64_t sh[256];
+  __shared__ uint32_t cnt_sh[4];
+  __shared__ uint64_t chunk_base;
+  const uint32_t t = threadIdx.x, g = blockIdx.x + 1u;
+  if (g == 1u && t == 0u) {
+    bounds[0] = 0u;
+    bounds[G] = static_cast<uint32_t>(n);
+  }
+  // chunk level: thread t holds chunks [b0, b1)
+  const uint32_t k = (nb + 255u) / 256u;
+  const uint32_t b0 = t * k < nb ? t * k : nb, b1 = b0 + k < nb ? b0 + k : nb;
+  uint64_t loc = 0;
+  for (uint32_t b = b0; b < b1; ++b) loc += sums[b];
+  uint64_t T = 0;
+  const uint64_t e0 = block_excl64(loc, sh, T);
+  const uint64_t target = (T / G) * g + (T % G) * g / G;
+  uint32_t cnt = 0;
+  uint64_t e = e0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    cnt += e < target ? 1u : 0u;
+    e += sums[b];
+  }
+  // chunks with excl < target: count over the block (>= 1: chunk 0 starts at 0)
+  uint32_t c = cnt;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((t & 63u) == 0u) cnt_sh[t >> 6] = c;
+  __syncthreads();
+  const uint32_t chunk = cnt_sh[0] + cnt_sh[1] + cnt_sh[2] + cnt_sh[3] - 1u;
+  if (chunk >= b0 && chunk < b1) {  // its owner: the chunk's exclusive weight
+    uint64_t x = e0;
+    for (uint32_t b = b0; b < chunk; ++b) x += sums[b];
+    chunk_base = x;
+  }
+  __syncthreads();
+  const uint64_t base_e = chunk_base;
+  __syncthreads();
+  // span level inside the chunk: thread t holds spans [s0, s1)
+  const uint64_t lo = static_cast<uint64_t>(chunk) * C;
+  const uint64_t hi = lo + C < n ? lo + C : n;
+  const uint64_t m = (hi - lo + 255u) / 256u;
+  const uint64_t s0 = lo + t * m < hi ? lo + t * m : hi, s1 = s0 + m < hi ? s0 + m : hi;
+  uint64_t w = 0;
+  for (uint64_t i = s0; i < s1; ++i) w += len[i] + 64u;
+  uint64_t T2 = 0;
+  uint64_t x = base_e + block_excl64(w, sh, T2);
+  uint32_t below = 0;
+  for (uint64_t i = s0; i < s1; ++i) {
+    below += x < target ? 1u : 0u;
+    x += len[i] + 64u;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) below += __shfl_xor(below, d, 64);
+  if ((t & 63u) == 0u) cnt_sh[t >> 6] = below;
+  __syncthreads();
+  if (t == 0u)
+    bounds[g] = static_cast<uint32_t>(lo) + cnt_sh[0] + cnt_sh[1] + cnt_sh[2] + cnt_sh[3];
+}
+
 }  // namespace util
 }  // namespace wipdb

@@ -38,7 +38,7 @@ namespace lk {
 template <int INIT>
 __global__ void crc32c_lds_spans_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                         const uint32_t*, uint32_t*, uint64_t, uint32_t,
-                                        const uint8_t*);
+                                        const uint8_t*, const uint32_t*);
 __global__ void crc32c_lds_strided_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t,
                                           uint32_t*, uint64_t, uint32_t, const uint8_t*);
 __global__ void crc32c_lds_verify_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
@@ -60,6 +60,9 @@ __global__ void check_spans_kernel(const uint64_t*, const uint32_t*, uint64_t, u
 __global__ void split_expand_kernel(const uint64_t*, const uint32_t*, const uint32_t*, uint64_t,
                                     uint32_t, uint32_t, uint32_t, uint64_t*, uint32_t*, uint32_t*,
                                     uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+__global__ void balance_sums_kernel(const uint32_t*, uint64_t, uint32_t, uint64_t*);
+__global__ void balance_bounds_kernel(const uint32_t*, uint64_t, uint32_t, const uint64_t*, uint32_t,
+                                      uint32_t, uint32_t*);
 __global__ void split_copy_kernel(const uint32_t*, const uint32_t*, uint32_t*, uint64_t, uint32_t);
 __global__ void split_combine_kernel(const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint32_t*, const uint32_t*, uint32_t*, uint64_t, uint32_t,
@@ -549,12 +552,36 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
       rc = LaunchClasses(ctx, static_cast<const uint8_t*>(base), off + pos, len + pos,
                          init ? init + pos : nullptr, out + pos, n, 0, mask, st);
     } else {
+      const int grid = LdsGrid(ctx, n);
+      // HCRC_BALANCE: byte-balanced contiguous workgroup ranges, two small
+      // passes over the length column first (only worth it where the spans'
+      // sizes vary: the static deal is exact for equal spans)
+      const bool bal = (flags & HCRC_BALANCE) != 0 && n >= size_t(64) * grid && grid > 1;
+      uint8_t* scratch = nullptr;
+      const uint32_t* bounds = nullptr;
+      if (bal) {
+        const size_t C = std::max<size_t>(1024, (n + 4095) / 4096 + 255) / 256 * 256;
+        const uint32_t nb = static_cast<uint32_t>((n + C - 1) / C);
+        const size_t bytes = size_t(nb) * 8 + (size_t(grid) + 1) * 4;
+        HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), bytes,
+                                          ctx->scratch_pool, st));
+        uint64_t* sums = reinterpret_cast<uint64_t*>(scratch);
+        uint32_t* bd = reinterpret_cast<uint32_t*>(scratch + size_t(nb) * 8);
+        hipLaunchKernelGGL(wipdb::util::balance_sums_kernel, dim3(nb), dim3(256), 0, st,
+                           len + pos, static_cast<uint64_t>(n), static_cast<uint32_t>(C), sums);
+        hipLaunchKernelGGL(wipdb::util::balance_bounds_kernel, dim3(grid - 1), dim3(256), 0, st,
+                           len + pos, static_cast<uint64_t>(n), static_cast<uint32_t>(C), sums,
+                           nb, static_cast<uint32_t>(grid), bd);
+        bounds = bd;
+      }
       hipLaunchKernelGGL(init ? lk::crc32c_lds_spans_kernel<1> : lk::crc32c_lds_spans_kernel<0>,
-                         dim3(LdsGrid(ctx, n)), dim3(lk::kThreads),
+                         dim3(grid), dim3(lk::kThreads),
                          lk::kLdsBytes, st, static_cast<const uint8_t*>(base), off + pos,
                          len + pos, init ? init + pos : nullptr, out + pos,
-                         static_cast<uint64_t>(n), mask ? lk::kFlagMask : 0u, ctx->d_image);
+                         static_cast<uint64_t>(n), mask ? lk::kFlagMask : 0u, ctx->d_image,
+                         bounds);
       rc = LaunchedLp(st);
+      if (scratch && hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
     }
     if (rc) return rc;
   }
@@ -1025,7 +1052,8 @@ int hcrc_ctx_device(hcrc_ctx* ctx) { return ctx ? ctx->device : -1; }
 int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const uint32_t* lengths,
                const uint32_t* init_crcs, uint32_t* out_crcs, size_t count, int flags) {
   if (!ctx || (count && (!base || !offsets || !lengths || !out_crcs))) return HCRC_ERR_INVALID;
-  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG))
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG |
+                HCRC_BALANCE))
     return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
   HCRC_DEVICE(ctx);
@@ -1047,7 +1075,8 @@ int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offset
                      const uint32_t* d_lengths, const uint32_t* d_init_crcs, uint32_t* d_out_crcs,
                      size_t count, int flags, void* stream) {
   if (!ctx || !(flags & HCRC_DEVICE_PTRS)) return HCRC_ERR_INVALID;
-  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG))
+  if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG |
+                HCRC_BALANCE))
     return HCRC_ERR_INVALID;
   if (count && (!d_base || !d_offsets || !d_lengths || !d_out_crcs)) return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
