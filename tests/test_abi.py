@@ -22,6 +22,20 @@ def test_library_exports_every_header_symbol():
     assert set(_lib._PROTOS) == set(syms)
 
 
+def test_header_flag_values_match_binding():
+    """Every HCRC_* value macro of include/hip_crc32c_batch.h that the
+    Python binding names (flags such as HCRC_BALANCE, error codes) has the
+    header's value."""
+    import re
+    hdr = open(os.path.join(REPO, "include", "hip_crc32c_batch.h")).read()
+    macros = {m.group(1): int(m.group(2), 0) for m in
+              re.finditer(r"#define (HCRC_[A-Z_]+) \(?(-?(?:0x)?[0-9A-Fa-f]+)\)?", hdr)}
+    named = {k: getattr(_lib, k) for k in macros if hasattr(_lib, k)}
+    assert {"HCRC_DEVICE_PTRS", "HCRC_SPLIT_SMALL", "HCRC_SPLIT_LONG", "HCRC_BALANCE"} <= set(named)
+    for k, v in named.items():
+        assert v == macros[k], (k, v, macros[k])
+
+
 def test_abi_version_and_strerror():
     lib = _lib.load()
     assert lib.hcrc_abi_version() == 1
