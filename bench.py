@@ -15,12 +15,16 @@ collective (blocks are independent) -- only the barrier and the max-time
 reduction of the contract.  value = total bytes of all ranks / max time.
 
 Before the W warmup steps the bench preconditions the card with untimed
-launches of the same step (at least --precondition-ms of GPU time, 80 by
+launches of the same step (at least --precondition-ms of GPU time, 250 by
 default) and checks that every one of them returns the same CRCs: right
 after idle, back-to-back launches of this kernel run up to 1.5x slower for
 the first ~30-60 ms while the SMU settles the power-capped clocks
 (profiles/r02_launch_series.json); the timed steps measure the steady state.
-The line says so ("precondition").
+The compare kernels torch uses for the check are loaded before the window
+(their first use cost ~250 ms of GPU idle inside it), so the
+window is continuous GPU work; the line reports the mean kernel time of the
+window's first and last 10 launches, so the settling is visible
+("precondition").
 
 Also printed in the same JSON line:
   roofline      the CRC kernel's average launch time from HIP events on the
@@ -40,6 +44,19 @@ Also printed in the same JSON line:
                 DRAM), and on every CPU this process may use; rank 0, N=1.
   parity        the reference CRCs vs the GPU's for every block of the shard
                 (N = 1) or a 64 Ki-block sample per rank (N > 1).
+  readstream_ceiling
+                this box's plain read-stream kernel over the same shard (the
+                same-box HBM ceiling), after the timed region; roofline
+                frac_of_readstream = achieved / its read rate.
+  config3_mixed, table_blocks, verified_table_blocks, config5_pcie
+                (rank 0, N = 1, after the headline; --no-extra skips them)
+                BASELINE configs[2] and [4] under the same clock: config 3's
+                Zipf-mixed SST-packed batch and its per-bucket GiB/s and p99
+                batch latency, WriteRawBlock-shaped table blocks and their
+                ReadBlock verify (device-resident), and config 5's 8Binsert
+                SST stream from pinned host memory (zero-copy, PCIe-inclusive)
+                against a measured PCIe H2D ceiling; every one sample-checked
+                against the reference's kv::crc32c (oracle/_ref).
 """
 from __future__ import annotations
 
@@ -65,7 +82,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)  # >= 50 back-to-back launches
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--precondition-ms", type=float, default=80.0,
+    p.add_argument("--precondition-ms", type=float, default=250.0,
                    help="untimed GPU time of same-step launches before the warmup (power "
                         "transient, see the docstring); 0 disables")
     p.add_argument("--blocks", type=int, default=0,
@@ -77,8 +94,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=5.0,
                    help="minimum time of the 1-thread reference baseline (whole passes)")
-    p.add_argument("--readstream", action="store_true",
-                   help="also time the read-stream ceiling kernel")
+    p.add_argument("--no-readstream", action="store_true",
+                   help="skip the read-stream ceiling kernel (timed after the headline)")
+    p.add_argument("--readstream", action="store_true", help=argparse.SUPPRESS)  # (the default)
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip configs 3 / 5 and the table-block shapes after the headline")
     return p.parse_args()
 
 
@@ -127,9 +147,7 @@ def cpu_check(host_blocks, gpu_crc, target_s, baseline: bool):
     out = np.empty(nblk, np.uint32)
     args = (host_blocks.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, out.ctypes.data)
     ncpu = usable_cpus()
-    t0 = time.perf_counter()
     fn(*args, nblk, 0, ncpu)
-    all_s = time.perf_counter() - t0
     mism = int((out != gpu_crc[:nblk]).sum())
     parity = {"blocks_checked": int(nblk), "mismatches": mism}
     if not baseline:
@@ -142,6 +160,15 @@ def cpu_check(host_blocks, gpu_crc, target_s, baseline: bool):
         if el >= target_s:
             break
     gib_s = passes * nblk * BLOCK / el / 2**30
+    # all usable CPUs, timed the same way (whole passes for >= target_s; the
+    # parity pass above was the warm one)
+    apasses, t0 = 0, time.perf_counter()
+    while True:
+        fn(*args, nblk, 0, ncpu)
+        apasses += 1
+        ael = time.perf_counter() - t0
+        if ael >= target_s:
+            break
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -156,9 +183,10 @@ def cpu_check(host_blocks, gpu_crc, target_s, baseline: bool):
         "sample": f"all {nblk} x 4 KiB blocks of rank 0's shard ({nblk * BLOCK >> 20} MiB, "
                   f"copied back from HBM, read from DRAM), {passes} pass(es) in {el:.1f} s, "
                   f"ref kv::crc32c::Extend per block",
-        "all_cores": {"value": round(nblk * BLOCK / all_s / 2**30, 3), "cores": ncpu,
-                      "note": "one pass over the same blocks on every CPU this job may use "
-                              "(affinity mask capped by OMP_NUM_THREADS)"},
+        "all_cores": {"value": round(apasses * nblk * BLOCK / ael / 2**30, 3), "cores": ncpu,
+                      "sample": f"{apasses} whole passes over the same blocks in {ael:.1f} s "
+                                f"after a warm pass, on every CPU this job may use (affinity "
+                                f"mask capped by OMP_NUM_THREADS)"},
         "host": {"cpu": cpu_model, "nproc": os.cpu_count(), "usable_cpus": ncpu,
                  "hostname": socket.gethostname()},
     }, parity
@@ -224,16 +252,25 @@ def main():
         e0.record(stream)
         step(scratch)
         e1.record(stream)
-        torch.cuda.synchronize(dev)
-        n = max(8, min(4096, int(a.precondition_ms / max(e0.elapsed_time(e1), 1e-3)) + 1))
         mism = torch.zeros((), dtype=torch.int64, device=dev)
+        mism += (scratch != ref).sum()  # torch's compare / reduce kernels loaded here
+        torch.cuda.synchronize(dev)
+        n = max(16, min(4096, int(a.precondition_ms / max(e0.elapsed_time(e1), 1e-3)) + 1))
+        pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(n)]
         e0.record(stream)
-        for _ in range(n):
+        for ps, pe in pev:
+            ps.record(stream)
             step(scratch)
+            pe.record(stream)
             mism += (scratch != ref).sum()
         e1.record(stream)
         torch.cuda.synchronize(dev)
+        pk = [ps.elapsed_time(pe) for ps, pe in pev]
         pre = {"launches": n + 2, "gpu_ms": round(e0.elapsed_time(e1), 2),
+               "kernel_ms_sum": round(sum(pk), 2),
+               "first10_kernel_ms": round(sum(pk[:10]) / 10, 4),
+               "last10_kernel_ms": round(sum(pk[-10:]) / 10, 4),
                "identical_outputs": int(mism.item()) == 0,
                "why": "after idle, back-to-back launches run up to 1.5x slower for ~30-60 ms while "
                       "the SMU settles the power-capped clocks (profiles/r02_launch_series.json)"}
@@ -271,7 +308,7 @@ def main():
     kern_avg_ms = max_over_ranks(kern_avg_ms, dev)
 
     rs = None
-    if a.readstream:
+    if not a.no_readstream:
         rs_out = torch.empty(nblk, dtype=torch.int32, device=dev)
         for _ in range(2):
             eng.readstream_device(data, BLOCK, BLOCK, nblk, rs_out, stream=stream.cuda_stream)
@@ -283,7 +320,9 @@ def main():
         torch.cuda.synchronize(dev)
         rs_ms = s0.elapsed_time(s1) / a.steps
         rs = {"kernel": "readstream_kernel", "avg_ms": round(rs_ms, 4),
-              "read_GBps": round(nblk * BLOCK / rs_ms / 1e6, 1)}
+              "read_GBps": round(nblk * BLOCK / rs_ms / 1e6, 1),
+              "what": "this box's plain read stream over the same shard, after the timed region"}
+        del rs_out
 
     # parity (and, rank 0 at N = 1, the CPU baseline) on the host
     gpu_crc = out.cpu().numpy().view(np.uint32)
@@ -298,6 +337,11 @@ def main():
         dist.all_reduce(t)
         par = {"blocks_checked": int(t[1].item()), "mismatches": int(t[0].item()),
                "scope": "64 Ki-block sample per rank"}
+
+    extra = {}
+    if rank == 0 and world == 1 and not a.no_extra:
+        from scripts.bench_configs import run_all
+        extra = run_all(eng, dev, stream, _ref_batch()[0])
 
     if rank == 0:
         total_bytes = world * nblk * BLOCK
@@ -342,9 +386,11 @@ def main():
         }
         if rs:
             line["readstream_ceiling"] = rs
+            line["roofline"]["frac_of_readstream"] = round(achieved / rs["read_GBps"], 4)
         if cb:
             line["cpu_baseline"] = cb
         line["parity"] = par
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

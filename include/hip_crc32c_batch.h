@@ -108,6 +108,19 @@ extern "C" {
  * stream-ordered scratch.  Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG
  * and for batches of fewer than 64 spans per workgroup. */
 #define HCRC_BALANCE 0x10
+/* SST-packed device batch (hcrc_batch_async / hcrc_batch with
+ * HCRC_DEVICE_PTRS): the caller says the spans are sorted by offset, do not
+ * overlap and leave gaps of less than 4 KiB -- what TableBuilder::
+ * WriteRawBlock leaves in a write buffer (kv/src/table/table_builder.cc:
+ * 183-202), a WAL block, config 3's stream.  The batch is then read as ONE
+ * byte stream, 4 KiB page by page, fully coalesced, each workgroup an equal
+ * share of the bytes (stream-tiled kernel).  A small
+ * pre-pass checks the promise (and that no 4 KiB holds more than 62 span
+ * starts); a batch that breaks it runs the default pipeline instead, so
+ * the flag can cost speed, never a CRC.  Scratch: (32 G + 9) * 4 bytes,
+ * stream-ordered.  Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG;
+ * HCRC_BALANCE is implied. */
+#define HCRC_PACKED 0x20
 
 typedef struct hcrc_ctx hcrc_ctx;
 
@@ -187,19 +200,22 @@ int hcrc_check_spans(hcrc_ctx* ctx, uint64_t base_bytes,
 /* In-kernel faults.  The lane-packed kernels never leave a span
  * uncomputed without saying so: a wait of the workgroup's long-span queue
  * that runs out of its bound (no schedule of a resident workgroup gets
- * there) sets a fault word instead.  The synchronous entry points
- * (hcrc_batch, hcrc_batch_multi*) check their own word and return
- * HCRC_ERR_KERNEL (outputs incomplete; the C++ ExtendBatch(kAuto) then
- * computes the batch on the CPU).  Launches on a caller's stream (the
- * *_async entry points) share the context's word: hcrc_ctx_check returns
- * HCRC_ERR_KERNEL if any of them reported a fault since the last check
- * (and clears it) -- call it after synchronising those streams.  The
+ * there) sets the launch's fault word instead.  Every launch writes the word
+ * of its owner only: a synchronous entry point (hcrc_batch,
+ * hcrc_batch_multi*) checks its own and returns HCRC_ERR_KERNEL (outputs
+ * incomplete; the C++ ExtendBatch(kAuto) then computes the batch on the
+ * CPU); the *_async entry points use one word per caller stream, which
+ * hcrc_sync(ctx, stream) reads and clears for that stream (a fault of a
+ * launch on another stream, or of a synchronous call, is never reported
+ * there).  hcrc_ctx_check reads and clears the words of every stream the
+ * context has launched on -- call it after synchronising them.  The
  * reference's Extend is infallible (kv/src/util/crc32c.h:24); a wrong CRC
  * returned as success is the one failure a checksum must never have. */
 int hcrc_ctx_check(hcrc_ctx* ctx);
 
 /* Wait for all work on `stream` (NULL = the HIP default stream), then
- * hcrc_ctx_check. */
+ * HCRC_ERR_KERNEL if a launch of this context on `stream` reported a fault
+ * since that stream's last check (the check clears it). */
 int hcrc_sync(hcrc_ctx* ctx, void* stream);
 
 /* Host-memory batch sharded over `ndev` devices by bytes, one host thread

@@ -22,22 +22,27 @@
 //     CompactionInput check every block of many tables in batches.
 //
 // The on-disk framing is the same as kv's (the 5-byte block trailer, the
-// 48-byte footer, kTableMagicNumber 0xdb4775248b80fb57): tests/cpp/
-// test_leveldb_adapter.cc writes tables through this adapter and the file
-// must equal the bytes the reference's kv::TableBuilder writes for the same
-// entries and options.  leveldb's OWN TableBuilder is not compiled here (its
-// port layer needs the CMake-generated port/port_config.h), so the
-// leveldb-side byte identity is parity-unpinned beyond that kv equivalence.
+// 48-byte footer, kTableMagicNumber 0xdb4775248b80fb57).  The index keys are
+// leveldb's: the builder shortens them with the leveldb::Options comparator
+// itself (ComparatorFrom wraps it), so tests/cpp/test_leveldb_adapter.cc's
+// tables equal, byte for byte, what leveldb's own TableBuilder writes for the
+// same entries and options (leveldb compiled in place, oracle/Makefile
+// LDB_SO; tests/test_table.py), and leveldb's Table::Open + ReadBlock accept
+// them.
 //
-// Only inline members of leveldb's headers are used, so including this file
-// links against no leveldb library.  SupportedOptions says whether a
-// leveldb::Options can be served (no compression -- WipDB's benchmarks run
-// without it, kv_bench.cc:984 -- a bytewise or internal-over-bytewise
-// comparator, no filter or the built-in bloom filter); call it first.
+// Apart from the comparator the adapter calls through (a leveldb deployment
+// links leveldb anyway), only inline members of leveldb's headers are used.
+// SupportedOptions says whether a leveldb::Options can be served (no
+// compression -- WipDB's benchmarks run without it, kv_bench.cc:984 -- and
+// no filter or the built-in bloom filter); call it first.
 #pragma once
 #include <string.h>
 
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <string_view>
 
 #include "leveldb/comparator.h"
 #include "leveldb/env.h"
@@ -70,40 +75,67 @@ class WritableFileSink : public table::TableSink {
   File* f_;
 };
 
+// wipdb::table's comparator interface over a leveldb::Comparator (or
+// anything with its Name / Compare / FindShortestSeparator /
+// FindShortSuccessor): the builder's index keys are then leveldb's own
+// (leveldb/table/table_builder.cc:106-107, 199-200 call the same two
+// functions), whatever the comparator -- bytewise, InternalKeyComparator
+// (db/dbformat.cc), or a user's.
+template <class Cmp = leveldb::Comparator>
+class ComparatorFrom : public table::Comparator {
+ public:
+  explicit ComparatorFrom(const Cmp* c) : c_(c) {}
+  const char* Name() const override { return c_->Name(); }
+  int Compare(std::string_view a, std::string_view b) const override {
+    return c_->Compare(leveldb::Slice(a.data(), a.size()), leveldb::Slice(b.data(), b.size()));
+  }
+  void FindShortestSeparator(std::string* start, std::string_view limit) const override {
+    c_->FindShortestSeparator(start, leveldb::Slice(limit.data(), limit.size()));
+  }
+  void FindShortSuccessor(std::string* key) const override { c_->FindShortSuccessor(key); }
+
+ private:
+  const Cmp* c_;
+};
+
+// One wrapper per leveldb comparator, for the life of the process
+// (comparators are long-lived: leveldb::BytewiseComparator() is a
+// singleton, a DB's InternalKeyComparator lives as long as the DB).
+template <class Cmp>
+inline const table::Comparator* WrapComparator(const Cmp* c) {
+  static std::mutex mu;
+  static auto* m = new std::map<const Cmp*, std::unique_ptr<ComparatorFrom<Cmp>>>;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& w = (*m)[c];
+  if (!w) w.reset(new ComparatorFrom<Cmp>(c));
+  return w.get();
+}
+
 // Whether wipdb::table can write what leveldb::TableBuilder would for these
 // options.  Anything else must stay on leveldb::TableBuilder, since
 // TableOptionsFrom would write a different (valid-looking) table:
 //   * no compression (the builder stores blocks raw);
-//   * comparator "leveldb.BytewiseComparator" (leveldb's default), or
-//     "leveldb.InternalKeyComparator" (leveldb/db/dbformat.cc:46-48) over a
-//     bytewise user comparator -- the wrapped comparator is not visible
-//     through leveldb's public headers, so the caller confirms it
-//     (internal_user_bytewise); index separators and successors are computed
-//     bytewise on the (user) key, any other order would misplace lookups;
 //   * no filter policy, or one named "leveldb.BuiltinBloomFilter2"
 //     (leveldb/util/bloom.cc; the InternalFilterPolicy wrapping it reports the
 //     same name, dbformat.cc:101-103): the meta entry "filter.<Name>" and the
 //     filter bytes are the built-in bloom filter's.
+// Any comparator is served: its own separators shorten the index keys.  A
+// comparator named "leveldb.InternalKeyComparator" means internal keys (the
+// bloom filter hashes the user key, as InternalFilterPolicy does); the second
+// argument is kept for source compatibility and no longer consulted.
 template <class Opts = leveldb::Options>
-inline bool SupportedOptions(const Opts& o, bool internal_user_bytewise = false) {
+inline bool SupportedOptions(const Opts& o, bool /*internal_user_bytewise*/ = false) {
   if (o.compression != leveldb::kNoCompression) return false;
-  const char* cmp = o.comparator ? o.comparator->Name() : "leveldb.BytewiseComparator";
-  if (strcmp(cmp, "leveldb.InternalKeyComparator") == 0) {
-    if (!internal_user_bytewise) return false;
-  } else if (strcmp(cmp, "leveldb.BytewiseComparator") != 0) {
-    return false;
-  }
   if (o.filter_policy && strcmp(o.filter_policy->Name(), "leveldb.BuiltinBloomFilter2") != 0)
     return false;
   return true;
 }
 
 // The table options a leveldb::Options stands for (only for options
-// SupportedOptions accepts).  leveldb::FilterPolicy
-// does not expose its bits per key, so the caller passes what it gave
-// NewBloomFilterPolicy (0 = no filter policy).  A comparator named
-// "leveldb.InternalKeyComparator" (leveldb/db/dbformat.cc) selects internal
-// keys and the InternalFilterPolicy's user-key hashing, as in kv.
+// SupportedOptions accepts).  leveldb::FilterPolicy does not expose its bits
+// per key, so the caller passes what it gave NewBloomFilterPolicy (0 = no
+// filter policy).  A null comparator is leveldb's default,
+// leveldb::BytewiseComparator().
 template <class Opts = leveldb::Options>
 inline table::TableOptions TableOptionsFrom(const Opts& o, int bloom_bits, table::CrcMode mode,
                                             int device = -1) {
@@ -113,8 +145,10 @@ inline table::TableOptions TableOptionsFrom(const Opts& o, int bloom_bits, table
   t.bloom_bits_per_key = o.filter_policy ? bloom_bits : 0;
   t.crc_mode = mode;
   t.device = device;
-  if (o.comparator && strcmp(o.comparator->Name(), "leveldb.InternalKeyComparator") == 0)
-    t = table::InternalKeyTableOptions(t);
+  const auto* c = o.comparator ? o.comparator : leveldb::BytewiseComparator();
+  if (strcmp(c->Name(), "leveldb.InternalKeyComparator") == 0)
+    t = table::InternalKeyTableOptions(t);  // (user-key bloom filter)
+  t.comparator = WrapComparator(c);
   return t;
 }
 

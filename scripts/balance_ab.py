@@ -23,7 +23,6 @@ def main():
     stream = torch.cuda.current_stream(d)
     rng = np.random.default_rng(42)
     nbytes = 2 << 30
-    dbuf = torch.empty(2 * nbytes, dtype=torch.uint8, device=d)
     shapes = {}
     o, l, _ = zipf_spans(rng, nbytes, BUCKETS)
     shapes["mix"] = (o, l)
@@ -36,11 +35,16 @@ def main():
     n4 = nbytes // 4096  # 512 Ki aligned 4 KiB blocks, and the headline's 1 Mi over 4 GiB
     shapes["4k"] = (np.arange(n4, dtype=np.uint64) * 4096, np.full(n4, 4096, np.uint32))
     shapes["4k_1M"] = (np.arange(2 * n4, dtype=np.uint64) * 4096, np.full(2 * n4, 4096, np.uint32))
+    # the buffer the shapes need, to the byte (the 1 Mi-block shape covers 4
+    # GiB); every shape's spans are checked against it once before timing
+    need = max(int(o[-1]) + int(l[-1]) for o, l in shapes.values())
+    dbuf = torch.empty(need, dtype=torch.uint8, device=d)
     res = {}
     with Engine(0) as eng:
         eng.fill_splitmix64_device(dbuf, 11, stream=stream.cuda_stream)
         for name, (o, l) in shapes.items():
             do, dl = dev(o, d), dev(l, d)
+            eng.check_spans(dbuf.numel(), do, dl)  # raises on a span past the buffer
             out0 = torch.empty(o.size, dtype=torch.int32, device=d)
             out1 = torch.empty(o.size, dtype=torch.int32, device=d)
             t = {"default": [], "balance": []}

@@ -96,6 +96,23 @@ inline void copy16(uint32_t dst, uint64_t src) {
 // Runs kernel() on `grid` workgroups of 1024 lane threads (one workgroup at
 // a time, as many as the device has CUs would run at once).
 template <class F>
+inline void launch_blocks(uint32_t grid, const std::vector<uint32_t>& blocks, F kernel) {
+  for (uint32_t b : blocks) {
+    Group g;
+    std::vector<std::thread> th;
+    th.reserve(1024);
+    for (uint32_t t = 0; t < 1024; ++t)
+      th.emplace_back([&, t] {
+        t_tid = t;
+        t_bid = b;
+        t_grid = grid;
+        t_group = &g;
+        kernel();
+      });
+    for (auto& x : th) x.join();
+  }
+}
+template <class F>
 inline void launch(uint32_t grid, F kernel) {
   for (uint32_t b = 0; b < grid; ++b) {
     Group g;
@@ -140,17 +157,23 @@ inline void lds_st_sync(uint32_t a, uint32_t v) { __atomic_store_n(lds_w(a), v, 
 // not overwrite a slot another lane has yet to read)
 inline void lgkm_wait() { emu::wave().bar.wait(); }
 inline void compiler_barrier() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+inline void lds_order() { emu::wave().bar.wait(); }
 template <class T>
 inline void loads_landed(T&) {}
 inline uint32_t vzero() { return 0u; }
+
+inline void global_or(uint32_t* a, uint32_t v) { __atomic_fetch_or(a, v, __ATOMIC_SEQ_CST); }
 
 // ---- faults ----
 // the fault bits of the launches (the device counts faulting waves instead)
 namespace emu {
 inline std::atomic<uint32_t> g_faults{0};
 }
-inline void report_fault(uint32_t bits) {
-  if (emu::lane() == 0u) emu::g_faults.fetch_or(bits);
+inline void report_fault(unsigned int* word, uint32_t bits) {
+  if (emu::lane() == 0u) {
+    emu::g_faults.fetch_or(bits);
+    if (word) __atomic_store_n(word, 1u, __ATOMIC_SEQ_CST);
+  }
 }
 // queue record g_hide_marker's marker reads as 0 (never written): forces the
 // popper's timeout (with a small WIPDB_LP_SPIN)

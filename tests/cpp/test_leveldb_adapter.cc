@@ -1,16 +1,17 @@
 // tests/cpp/test_leveldb_adapter.cc -- the leveldb/table adapter
-// (include/wipdb_compat/leveldb_table_sink.h) compiled against leveldb's own
-// public headers (/root/reference/leveldb/include; no leveldb source is
-// compiled or linked -- its port layer needs a generated header):
+// (include/wipdb_compat/leveldb_table_sink.h) on leveldb's real types: built
+// by oracle/Makefile against leveldb's headers and leveldb's table code
+// compiled in place (libref_leveldb.so: BytewiseComparator,
+// InternalKeyComparator, the built-in bloom filter), so the GPU box runs it
+// prebuilt:
 //
-//   * Instantiate() type-checks the adapter on the real leveldb::WritableFile,
+//   * Instantiate() type-checks the adapter on leveldb::WritableFile,
 //     leveldb::Options and leveldb::RandomAccessFile (compiled, never run);
 //   * main() writes one table through WritableFileSink + TableOptionsFrom
-//     (a file type with leveldb::WritableFile's Append / Flush, an options
-//     struct with leveldb::Options's fields), reads it back through
-//     ReadImage and VerifyTable, and writes the bytes out for
-//     tests/test_table.py to compare with the reference's kv::TableBuilder
-//     under the same options (the leveldb and kv formats coincide).
+//     (a leveldb::Options with leveldb's own comparator and filter policy),
+//     reads it back through ReadImage and VerifyTable, and writes the bytes
+//     out for tests/test_table.py to compare with leveldb's own
+//     TableBuilder (and to have leveldb's Table::Open + ReadBlock verify).
 //
 // Usage: test_leveldb_adapter <entries.bin> <out.sst> <block_size> <restart>
 //                             <bloom_bits> <internal 0|1> <crc_mode 0..3>
@@ -22,6 +23,7 @@
 #include <string>
 #include <vector>
 
+#include "db/dbformat.h"  // leveldb::InternalKeyComparator, InternalFilterPolicy
 #include "wipdb_compat/leveldb_table_sink.h"
 
 namespace {
@@ -32,7 +34,7 @@ __attribute__((used)) void Instantiate(leveldb::WritableFile* f, const leveldb::
   wipdb::leveldbcompat::WritableFileSink<> sink(f);
   wipdb::table::TableBuilder tb(
       wipdb::leveldbcompat::TableOptionsFrom(*o, 10, wipdb::table::CrcMode::kBatchAuto), &sink);
-  (void)wipdb::leveldbcompat::SupportedOptions(*o, true);
+  (void)wipdb::leveldbcompat::SupportedOptions(*o);
   (void)wipdb::leveldbcompat::ReadImage(r, 100, img);
 }
 
@@ -59,21 +61,11 @@ struct MemRandom {
     return leveldb::Status::OK();
   }
 };
-struct NamedComparator {
-  const char* name;
-  const char* Name() const { return name; }
-};
-struct NamedPolicy {
-  const char* name;
-  const char* Name() const { return name; }
-};
-// leveldb::Options's fields the adapter reads
-struct Opts {
-  size_t block_size;
-  int block_restart_interval;
-  const NamedPolicy* filter_policy;
-  const NamedComparator* comparator;
-  leveldb::CompressionType compression;
+// a filter policy the adapter must refuse (not the built-in bloom filter)
+struct PrefixPolicy : leveldb::FilterPolicy {
+  const char* Name() const override { return "my.PrefixFilter"; }
+  void CreateFilter(const leveldb::Slice*, int, std::string*) const override {}
+  bool KeyMayMatch(const leveldb::Slice&, const leveldb::Slice&) const override { return true; }
 };
 
 }  // namespace
@@ -100,33 +92,32 @@ int main(int argc, char** argv) {
   };
   const uint32_t n = u32();
   const int bloom = atoi(argv[5]);
-  const NamedComparator icmp{"leveldb.InternalKeyComparator"}, bcmp{"leveldb.BytewiseComparator"};
-  static const NamedPolicy kBloom{"leveldb.BuiltinBloomFilter2"};
+  const leveldb::FilterPolicy* bloomp = bloom ? leveldb::NewBloomFilterPolicy(bloom) : nullptr;
+  const leveldb::InternalKeyComparator icmp(leveldb::BytewiseComparator());
+  const leveldb::InternalFilterPolicy ipol(bloomp);
   const bool internal = atoi(argv[6]) != 0;
-  Opts o{static_cast<size_t>(atol(argv[3])), atoi(argv[4]), bloom ? &kBloom : nullptr,
-         internal ? &icmp : &bcmp, leveldb::kNoCompression};
+  leveldb::Options o;  // what a leveldb DB / table user passes
+  o.block_size = static_cast<size_t>(atol(argv[3]));
+  o.block_restart_interval = atoi(argv[4]);
+  o.compression = leveldb::kNoCompression;
+  o.comparator = internal ? static_cast<const leveldb::Comparator*>(&icmp)
+                          : leveldb::BytewiseComparator();
+  o.filter_policy = bloomp ? (internal ? static_cast<const leveldb::FilterPolicy*>(&ipol) : bloomp)
+                           : nullptr;
   const auto mode = static_cast<wipdb::table::CrcMode>(atoi(argv[7]));
-  if (!wipdb::leveldbcompat::SupportedOptions(o, true)) return 3;
-  // options the adapter must refuse: compression, a custom
-  // comparator, an internal comparator whose user comparator is not
-  // confirmed bytewise, a filter policy other than the built-in bloom filter
-  Opts bad = o;
+  if (!wipdb::leveldbcompat::SupportedOptions(o)) return 3;
+  // options the adapter must refuse: compression, a filter policy other than
+  // the built-in bloom filter (any comparator is served: its own separators)
+  leveldb::Options bad = o;
   bad.compression = leveldb::kSnappyCompression;
-  if (wipdb::leveldbcompat::SupportedOptions(bad, true)) return 3;
-  static const NamedComparator rev{"leveldb.ReverseBytewiseComparator"};
-  bad = o;
-  bad.comparator = &rev;
-  if (wipdb::leveldbcompat::SupportedOptions(bad, true)) return 3;
-  bad = o;
-  bad.comparator = &icmp;
-  if (wipdb::leveldbcompat::SupportedOptions(bad, false)) return 3;
-  static const NamedPolicy custom{"my.PrefixFilter"};
+  if (wipdb::leveldbcompat::SupportedOptions(bad)) return 3;
+  static const PrefixPolicy custom;
   bad = o;
   bad.filter_policy = &custom;
-  if (wipdb::leveldbcompat::SupportedOptions(bad, true)) return 3;
+  if (wipdb::leveldbcompat::SupportedOptions(bad)) return 3;
   bad = o;
-  bad.comparator = nullptr;  // leveldb's default: bytewise
-  if (!internal && !wipdb::leveldbcompat::SupportedOptions(bad, false)) return 3;
+  bad.comparator = nullptr;  // (leveldb's default: bytewise)
+  if (!wipdb::leveldbcompat::SupportedOptions(bad)) return 3;
 
   MemFile file;
   wipdb::leveldbcompat::WritableFileSink<MemFile> sink(&file);

@@ -19,7 +19,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
+#include <algorithm>
 #include <random>
 #include <string>
 #include <vector>
@@ -38,6 +40,9 @@ uint32_t Extend(uint32_t init, const uint8_t* p, size_t n) {
 }
 
 int g_fail = 0;
+// the launches' fault word (every launch must leave it 0, except the forced
+// queue timeout, which must set it)
+unsigned int g_fault_word = 0;
 // the pipeline the next launches must choose (1 run_ea, 2 run_lp, 0 any)
 uint32_t g_want_pipe = 0;
 
@@ -67,7 +72,7 @@ void Report(const char* name, const std::vector<uint32_t>& got, const std::vecto
   }
   const uint64_t bs = emu::g_bad_src.exchange(0);
   if (bs) fprintf(stderr, "  %s: DMA source %#llx outside the buffer\n", name, (unsigned long long)(bs & ~1ull));
-  const uint32_t fb = emu::g_faults.exchange(0);
+  const uint32_t fb = emu::g_faults.exchange(0) | (__atomic_exchange_n(&g_fault_word, 0u, __ATOMIC_SEQ_CST) ? 0x80000000u : 0u);
   if (fb) fprintf(stderr, "  %s: the launch reported fault bits %#x\n", name, fb);
   const uint32_t pipes = emu::g_pipes.exchange(0);
   const bool pipe_bad =
@@ -120,10 +125,10 @@ void RunSpans(const char* name, std::vector<uint8_t>& buf, const std::vector<uin
   emu::launch(Grid(n, cus), [&] {
     if (inits)
       crc32c_lds_spans_kernel<1>(buf.data(), offs.data(), lens.data(), inits->data(), got.data(), n,
-                                 mask ? kFlagMask : 0u, img, bd);
+                                 mask ? kFlagMask : 0u, img, bd, &g_fault_word);
     else
       crc32c_lds_spans_kernel<0>(buf.data(), offs.data(), lens.data(), nullptr, got.data(), n,
-                                 mask ? kFlagMask : 0u, img, bd);
+                                 mask ? kFlagMask : 0u, img, bd, &g_fault_word);
   });
   Report(name, got, want, offs, lens);
 }
@@ -148,7 +153,7 @@ void RunVerify(const char* name, std::vector<uint8_t>& buf, const std::vector<ui
   SetRange(buf);
   const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
   emu::launch(Grid(n, cus), [&] {
-    crc32c_lds_verify_kernel(buf.data(), offs.data(), hl.data(), st.data(), n, img);
+    crc32c_lds_verify_kernel(buf.data(), offs.data(), hl.data(), st.data(), n, img, &g_fault_word);
   });
   std::vector<uint32_t> got(st.begin(), st.end());
   Report(name, got, want, offs, lens);
@@ -169,7 +174,7 @@ void RunStrided(const char* name, std::vector<uint8_t>& buf, uint64_t stride, ui
   const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
   emu::launch(Grid(n, cus), [&] {
     crc32c_lds_strided_kernel(buf.data(), stride, len, init, got.data(), n, mask ? kFlagMask : 0u,
-                              img);
+                              img, &g_fault_word);
   });
   Report(name, got, want, offs, lens);
 }
@@ -182,6 +187,170 @@ std::vector<uint64_t> Packed(const std::vector<uint32_t>& lens, uint64_t start, 
     cur += lens[i] + gap;
   }
   return o;
+}
+
+// A buffer of exactly `bytes` bytes whose last byte is followed by a PROT_NONE
+// page (and whose first page is preceded by one): a read of the emulated
+// kernel past the end of the data, a descriptor column or the output faults
+// the test process.  Untouched pages cost no memory (MAP_NORESERVE), so a
+// 2 GiB data buffer of which one workgroup's 8 MiB is written is cheap.
+template <class T>
+struct Guarded {
+  uint8_t* map = nullptr;
+  size_t maplen = 0;
+  T* p = nullptr;
+  size_t n = 0;
+  explicit Guarded(size_t count) : n(count) {
+    const size_t pg = 4096, bytes = count * sizeof(T), body = (bytes + pg - 1) / pg * pg;
+    maplen = body + 2 * pg;
+    void* m = mmap(nullptr, maplen, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
+                   -1, 0);
+    if (m == MAP_FAILED) abort();
+    map = static_cast<uint8_t*>(m);
+    mprotect(map, pg, PROT_NONE);
+    mprotect(map + pg + body, pg, PROT_NONE);
+    p = reinterpret_cast<T*>(map + pg + body - bytes);
+  }
+  ~Guarded() { munmap(map, maplen); }
+  Guarded(const Guarded&) = delete;
+  Guarded& operator=(const Guarded&) = delete;
+  T& operator[](size_t i) { return p[i]; }
+};
+
+// An exact-fit launch (verdict r4 item 1): spans whose last one ends at the
+// last byte of the data buffer, every column exactly `n` entries, each
+// followed by a guard page; the DMA range is the data's own pages.  Runs the
+// workgroups `blocks` of a `grid` launch (the last workgroup holds the last
+// span under both deals) and checks their spans.  verify: ReadBlock spans
+// (lens = handle sizes; the +1 type byte and the trailer are in the data).
+void RunExact(const char* name, Guarded<uint8_t>& data, const std::vector<uint64_t>& offs_v,
+              const std::vector<uint32_t>& lens_v, bool verify, bool balance, uint32_t grid,
+              const std::vector<uint32_t>& blocks) {
+  const size_t n = offs_v.size();
+  Guarded<uint64_t> off(n);
+  Guarded<uint32_t> len(n);
+  for (size_t i = 0; i < n; ++i) off[i] = offs_v[i], len[i] = lens_v[i];
+  // the spans the chosen workgroups own (both deals of crc32c_dev.h wg_units)
+  std::vector<uint32_t> bounds;
+  if (balance) {
+    std::vector<uint32_t> w(lens_v);
+    if (verify)
+      for (auto& x : w) x += 1u;
+    bounds = BalanceBounds(w, grid);
+  }
+  std::vector<uint8_t> mine(n, 0);
+  for (uint32_t g : blocks) {
+    if (balance) {
+      for (uint32_t s = bounds[g]; s < bounds[g + 1]; ++s) mine[s] = 1;
+    } else {
+      const uint64_t full = n / (16u * grid) * 16u;
+      for (uint64_t u = 0; u < full; ++u) mine[((u >> 4) * grid + g) * 16u + (u & 15u)] = 1;
+      for (uint64_t u = full; u * grid + g < n; ++u) mine[u * grid + g] = 1;
+    }
+  }
+  std::vector<uint32_t> want(n, 0x5A5A5A5Au);
+  size_t owned = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (!mine[i]) continue;
+    ++owned;
+    const uint32_t c = Extend(0u, data.p + offs_v[i], lens_v[i] + (verify ? 1u : 0u));
+    if (verify) {
+      uint32_t m;
+      memcpy(&m, data.p + offs_v[i] + lens_v[i] + 1u, 4);
+      want[i] = m == wipdb::gf2::Mask(c) ? 1u : 0u;
+    } else {
+      want[i] = c;
+    }
+  }
+  const uint64_t lo = reinterpret_cast<uint64_t>(data.p);
+  emu::g_src_lo = lo & ~uint64_t(4095);
+  emu::g_src_hi = lo + data.n;  // the data ends at a page boundary
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
+  std::vector<uint32_t> got(n, 0x5A5A5A5Au);
+  if (verify) {
+    Guarded<uint8_t> st(n);
+    for (size_t i = 0; i < n; ++i) st[i] = 0x5A;
+    emu::launch_blocks(grid, blocks, [&] {
+      crc32c_lds_verify_kernel(data.p, off.p, len.p, st.p, n, img, &g_fault_word);
+    });
+    for (size_t i = 0; i < n; ++i) got[i] = st[i] == 0x5A ? 0x5A5A5A5Au : st[i];
+    (void)balance;  // the verify entry point has no balanced deal
+  } else {
+    Guarded<uint32_t> out(n);
+    for (size_t i = 0; i < n; ++i) out[i] = 0x5A5A5A5Au;
+    emu::launch_blocks(grid, blocks, [&] {
+      crc32c_lds_spans_kernel<0>(data.p, off.p, len.p, nullptr, out.p, n, 0u, img,
+                                 balance ? bounds.data() : nullptr, &g_fault_word);
+    });
+    for (size_t i = 0; i < n; ++i) got[i] = out[i];
+  }
+  char label[96];
+  snprintf(label, sizeof label, "%s (%zu owned)", name, owned);
+  Report(label, got, want, offs_v, lens_v);
+}
+
+// HCRC_PACKED: the pre-pass (crc32c_ps_index_kernel) then the packed kernel
+// (run_ps, or run_lp when the pre-pass finds the batch not packed), on
+// `data` (any buffer; the DMA range is its pages).  C: chunks of the launch
+// (0: 32 per workgroup, as the host picks).  want_packed: what the pre-pass
+// must decide.
+void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std::vector<uint64_t>& offs,
+               const std::vector<uint32_t>& lens, const std::vector<uint32_t>* inits, bool mask,
+               uint32_t cus, uint32_t C, bool want_packed) {
+  // the data on whole pages of its own, at the same page offset (the kernel
+  // may read any byte of a page that holds a span byte; ASan builds of this
+  // test see a heap buffer's page neighbours as foreign)
+  const size_t pofs = reinterpret_cast<uintptr_t>(data0) & 4095u;
+  const size_t pbytes = (pofs + data_n + 4095u) & ~size_t(4095);
+  void* pm = nullptr;
+  if (posix_memalign(&pm, 4096, pbytes) != 0) abort();
+  memcpy(static_cast<uint8_t*>(pm) + pofs, data0, data_n);
+  struct Free { void* p; ~Free() { free(p); } } free_pm{pm};
+  const uint8_t* data = static_cast<const uint8_t*>(pm) + pofs;
+  const size_t n = offs.size();
+  const uint32_t grid = Grid(n, cus);
+  if (C == 0) C = 32u * grid;
+  std::vector<uint32_t> want(n), got(n, 0x5A5A5A5Au);
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t c = Extend(inits ? (*inits)[i] : 0u, data + offs[i], lens[i]);
+    want[i] = mask ? wipdb::gf2::Mask(c) : c;
+  }
+  std::vector<uint32_t> first(C + 1, 0xFFFFFFFFu), meta(kPsMetaWords, 0u);
+  const uint32_t pgrid = static_cast<uint32_t>(std::min<size_t>((n + 255) / 256, 8));
+  emu::launch(pgrid ? pgrid : 1, [&] {
+    crc32c_ps_index_kernel(offs.data(), lens.data(), n, C, first.data(), meta.data());
+  });
+  const bool packed = meta[0] == 0u;
+  if (packed)
+    for (uint32_t c = 0; c <= C; ++c)
+      if (first[c] > n || (c && first[c] < first[c - 1])) {
+        fprintf(stderr, "  %s: first[%u] = %u\n", name, c, first[c]);
+        ++g_fail;
+        return;
+      }
+  const uint64_t lo = reinterpret_cast<uint64_t>(data);
+  emu::g_src_lo = lo & ~uint64_t(4095);
+  emu::g_src_hi = (lo + data_n + 4095) & ~uint64_t(4095);
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
+  emu::launch(grid, [&] {
+    if (inits)
+      crc32c_lds_packed_kernel<1>(data, offs.data(), lens.data(), inits->data(), got.data(), n,
+                                  mask ? kFlagMask : 0u, img, first.data(), meta.data(), C,
+                                  &g_fault_word);
+    else
+      crc32c_lds_packed_kernel<0>(data, offs.data(), lens.data(), nullptr, got.data(), n,
+                                  mask ? kFlagMask : 0u, img, first.data(), meta.data(), C,
+                                  &g_fault_word);
+  });
+  char label[96];
+  snprintf(label, sizeof label, "%s [%s]", name, packed ? "ps" : "fallback");
+  if (packed != want_packed) {
+    fprintf(stderr, "  %s: the pre-pass says %s (meta %#x)\n", name, packed ? "packed" : "not packed",
+            meta[0]);
+    ++g_fail;
+  }
+  emu::g_pipes.exchange(0);
+  Report(label, got, want, offs, lens);
 }
 
 bool Want(int argc, char** argv, const char* name) {
@@ -328,14 +497,15 @@ int main(int argc, char** argv) {
     const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
     emu::launch(1, [&] {
       crc32c_lds_spans_kernel<0>(buf.data(), o.data(), l.data(), nullptr, got.data(), l.size(), 0u,
-                                 img, nullptr);
+                                 img, nullptr, &g_fault_word);
     });
     emu::g_spin = 1u << 22;
     emu::g_hide_marker = ~0u;
     size_t lost = 0;
     for (size_t i = 0; i < l.size(); ++i) lost += got[i] != want[i];
     const uint32_t fb = emu::g_faults.exchange(0);
-    const bool ok = (fb & kFaultQueuePop) != 0 && lost >= 1 && lost <= 4 &&
+    const bool word = __atomic_exchange_n(&g_fault_word, 0u, __ATOMIC_SEQ_CST) != 0u;
+    const bool ok = (fb & kFaultQueuePop) != 0 && word && lost >= 1 && lost <= 4 &&
                     emu::g_bad_src.exchange(0) == 0;
     printf("%-34s %6zu spans  %s (fault bits %#x, %zu lost)\n", "queue timeout: fault reported",
            l.size(), ok ? "ok" : "FAIL", fb, lost);
@@ -392,6 +562,176 @@ int main(int argc, char** argv) {
     RunStrided("strided 4096 masked", buf, 4096, 4096, 0, 255, 2, true);
     RunStrided("strided 4101 / 4097 masked (init)", buf, 4101, 4097, 0x12345678u, 255, 2, true);
     RunStrided("strided 4096 / 100 masked (init)", buf, 4096, 100, 7, 255, 2, true);
+  }
+  {
+    // Every buffer ends at a guard page: data, descriptor columns, outputs.
+    auto fill = [](Guarded<uint8_t>& d, uint64_t seed) {
+      uint64_t x = seed;
+      for (size_t i = 0; i + 8 <= d.n; i += 8) {
+        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        memcpy(d.p + i, &z, 8);
+      }
+    };
+    if (Want(argc, argv, "exact fit 2 GiB")) {
+      // the r04an shape: 512 Ki aligned 4 KiB blocks filling exactly 2 GiB,
+      // a 256-workgroup launch, its first and last workgroups, both deals
+      const size_t n = size_t(1) << 19;
+      Guarded<uint8_t> d(n * 4096);
+      fill(d, 11);
+      std::vector<uint64_t> o(n);
+      for (size_t i = 0; i < n; ++i) o[i] = 4096u * i;
+      const std::vector<uint32_t> l(n, 4096u);
+      RunExact("exact fit 2 GiB 4 KiB, round robin", d, o, l, false, false, 256, {0, 255});
+      RunExact("exact fit 2 GiB 4 KiB, balanced", d, o, l, false, true, 256, {0, 255});
+    }
+    if (Want(argc, argv, "exact fit verify 4 KiB")) {
+      // ReadBlock's 4 KiB blocks (4091 + type + trailer), the last trailer
+      // at the end; every 5th block corrupted
+      const size_t n = 16384;
+      Guarded<uint8_t> d(n * 4096);
+      fill(d, 12);
+      std::vector<uint64_t> o(n);
+      for (size_t i = 0; i < n; ++i) {
+        o[i] = 4096u * i;
+        uint32_t m = wipdb::gf2::Mask(Extend(0u, d.p + o[i], 4092));
+        if (i % 5 == 4) m ^= 1u << (i % 32);
+        memcpy(d.p + o[i] + 4092, &m, 4);
+      }
+      RunExact("exact fit verify 4 KiB", d, o, std::vector<uint32_t>(n, 4091u), true, false, 256,
+               {0, 255});
+    }
+    auto packed_exact = [&](const char* name, uint32_t lo, uint32_t hi, uint32_t gap, size_t n,
+                            bool verify) {
+      auto l = lens_of(n, lo, hi);
+      const auto o = Packed(l, 0, gap + (verify ? 5u : 0u));
+      const size_t end = o.back() + l.back() + (verify ? 5u : 0u);
+      Guarded<uint8_t> d(end);
+      fill(d, lo + hi);
+      if (verify) {
+        for (size_t i = 0; i < n; ++i) {
+          uint32_t m = wipdb::gf2::Mask(Extend(0u, d.p + o[i], l[i] + 1u));
+          if (i % 7 == 6) m ^= 0x100u;
+          memcpy(d.p + o[i] + l[i] + 1u, &m, 4);
+        }
+      }
+      const uint32_t grid = Grid(n, 3);
+      std::vector<uint32_t> all(grid);
+      for (uint32_t g = 0; g < grid; ++g) all[g] = g;
+      std::string s = std::string(name) + ", round robin";
+      RunExact(s.c_str(), d, o, l, verify, false, grid, all);
+      if (!verify) {
+        s = std::string(name) + ", balanced";
+        RunExact(s.c_str(), d, o, l, false, true, grid, all);
+      }
+    };
+    if (Want(argc, argv, "exact fit packed")) {
+      packed_exact("exact fit packed table blocks", 4097, 4225, 4, 1500, false);
+      packed_exact("exact fit packed verify table blocks", 4096, 4224, 0, 1500, true);
+      packed_exact("exact fit packed 512 B..2 KiB", 512, 2200, 5, 3000, false);
+      packed_exact("exact fit packed verify 300..5000", 300, 5000, 0, 1500, true);
+      packed_exact("exact fit packed 16..64 KiB", 16384, 65536, 5, 300, false);
+    }
+  }
+  if (Want(argc, argv, "packed tiny")) {  // single spans and pairs, one window or two
+    RunPacked("packed tiny one 4096", buf.data(), buf.size(), {0}, {4096}, nullptr, false, 1, 0, true);
+    RunPacked("packed tiny one 2000", buf.data(), buf.size(), {0}, {2000}, nullptr, false, 1, 0, true);
+    RunPacked("packed tiny one 2000 at 8", buf.data(), buf.size(), {8}, {2000}, nullptr, false, 1, 0, true);
+    RunPacked("packed tiny one 2001 at 9", buf.data(), buf.size(), {9}, {2001}, nullptr, false, 1, 0, true);
+    RunPacked("packed tiny two", buf.data(), buf.size(), {0, 2005}, {2000, 1500}, nullptr, false, 1, 0, true);
+    RunPacked("packed tiny one 8192", buf.data(), buf.size(), {0}, {8192}, nullptr, false, 1, 0, true);
+    RunPacked("packed tiny one 6000 at 3", buf.data(), buf.size(), {3}, {6000}, nullptr, false, 1, 0, true);
+  }
+  if (Want(argc, argv, "packed batches")) {
+    // HCRC_PACKED batches (crc32c_ps.h): SST-packed shapes on run_ps, and
+    // batches the pre-pass must refuse (the lane-packed fallback)
+    auto gaps = [&](const std::vector<uint32_t>& l, uint64_t start, uint32_t glo, uint32_t ghi) {
+      std::vector<uint64_t> o(l.size());
+      uint64_t cur = start;
+      for (size_t i = 0; i < l.size(); ++i) {
+        o[i] = cur;
+        cur += l[i] + glo + static_cast<uint32_t>(rng() % (ghi - glo + 1));
+      }
+      return o;
+    };
+    {
+      auto l = lens_of(3000, 512, 2200);
+      RunPacked("packed 512 B..2 KiB", buf.data(), buf.size(), Packed(l, 3, 5), l, nullptr, false, 3, 0,
+                true);
+      auto in = inits_of(l.size());
+      RunPacked("packed 512 B..2 KiB (inits, mask)", buf.data(), buf.size(), Packed(l, 6, 5), l, &in,
+                true, 2, 0, true);
+    }
+    {
+      auto l = lens_of(1500, 4097, 4225);
+      RunPacked("packed table blocks", buf.data(), buf.size(), Packed(l, 0, 4), l, nullptr, true, 3, 0,
+                true);
+    }
+    {
+      std::vector<uint64_t> o;
+      for (int i = 0; i < 2000; ++i) o.push_back(4096u * i);
+      RunPacked("packed aligned 4 KiB", buf.data(), buf.size(), o, std::vector<uint32_t>(2000, 4096),
+                nullptr, false, 3, 0, true);
+    }
+    {
+      const uint32_t B[] = {512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+      std::vector<uint32_t> l;
+      uint64_t tot = 0;
+      while (tot < (18u << 20)) {
+        const uint32_t b = B[rng() % 8 < 5 ? rng() % 4 : 4 + rng() % 4];
+        l.push_back(b + static_cast<uint32_t>(rng() % (b / 8 + 1)));
+        tot += l.back() + 5;
+      }
+      auto in = inits_of(l.size());
+      RunPacked("packed mix 512 B..72 KiB (inits)", buf.data(), buf.size(), Packed(l, 1, 5), l, &in,
+                false, 4, 0, true);
+      RunPacked("packed mix, 4 KiB chunks", buf.data(), buf.size(), Packed(l, 7, 5), l, nullptr, true,
+                3, 4000, true);
+    }
+    {
+      // short and empty spans among the stream ones, ragged gaps 0..300,
+      // spans of exactly 64 / 65 bytes, words shared across a 0..3-byte gap
+      std::vector<uint32_t> l;
+      for (int i = 0; i < 2500; ++i) {
+        const uint32_t r = static_cast<uint32_t>(rng() % 20);
+        l.push_back(r == 0 ? 0u : r == 1 ? 1u + static_cast<uint32_t>(rng() % 63)
+                   : r == 2 ? 64u : r == 3 ? 65u : 64u + static_cast<uint32_t>(rng() % 3000));
+      }
+      auto in = inits_of(l.size());
+      RunPacked("packed shorts, empties, 64 B, gaps 0..300", buf.data(), buf.size(), gaps(l, 5, 0, 300),
+                l, &in, true, 3, 0, true);
+      RunPacked("packed tight gaps 0..3", buf.data(), buf.size(), gaps(l, 2, 0, 3), l, nullptr, false, 3,
+                0, true);
+      RunPacked("packed gaps up to 4095, small chunks", buf.data(), buf.size(), gaps(l, 9, 0, 4095),
+                  l, &in, false, 2, 700, true);
+    }
+    {
+      // exact fit: the last span's last byte is the buffer's last byte
+      auto l = lens_of(2000, 700, 5000);
+      const auto o = Packed(l, 0, 4);
+      Guarded<uint8_t> d(o.back() + l.back());
+      for (size_t i = 0; i < d.n; ++i) d[i] = static_cast<uint8_t>(rng());
+      RunPacked("packed exact fit", d.p, d.n, o, l, nullptr, true, 3, 0, true);
+    }
+    {
+      // not packed: the fallback computes them all the same
+      auto l = lens_of(2000, 300, 3000);
+      auto o = Packed(l, 3, 5);
+      std::swap(o[100], o[101]);
+      std::swap(l[100], l[101]);
+      RunPacked("not packed: unsorted", buf.data(), buf.size(), o, l, nullptr, false, 3, 0, false);
+      auto o2 = Packed(l, 3, 5);
+      o2[500] -= 10;  // overlaps the span before
+      RunPacked("not packed: overlap", buf.data(), buf.size(), o2, l, nullptr, false, 3, 0, false);
+      auto o3 = Packed(l, 3, 5);
+      for (size_t i = 700; i < o3.size(); ++i) o3[i] += 5000;  // a gap of 5 KiB
+      RunPacked("not packed: a 5 KiB gap", buf.data(), buf.size(), o3, l, nullptr, false, 3, 0, false);
+      auto l4 = lens_of(3000, 5, 60);
+      RunPacked("not packed: dense short spans", buf.data(), buf.size(), Packed(l4, 1, 7), l4, nullptr,
+                false, 3, 0, false);
+    }
   }
   printf("%s: %d failing cases\n", g_fail ? "FAIL" : "PASS", g_fail);
   return g_fail ? 1 : 0;

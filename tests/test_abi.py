@@ -31,7 +31,8 @@ def test_header_flag_values_match_binding():
     macros = {m.group(1): int(m.group(2), 0) for m in
               re.finditer(r"#define (HCRC_[A-Z_]+) \(?(-?(?:0x)?[0-9A-Fa-f]+)\)?", hdr)}
     named = {k: getattr(_lib, k) for k in macros if hasattr(_lib, k)}
-    assert {"HCRC_DEVICE_PTRS", "HCRC_SPLIT_SMALL", "HCRC_SPLIT_LONG", "HCRC_BALANCE"} <= set(named)
+    assert {"HCRC_DEVICE_PTRS", "HCRC_SPLIT_SMALL", "HCRC_SPLIT_LONG", "HCRC_BALANCE",
+            "HCRC_PACKED"} <= set(named)
     for k, v in named.items():
         assert v == macros[k], (k, v, macros[k])
 
@@ -159,7 +160,15 @@ def test_lane_packed_kernels_emulated(tmp_path):
     # pipeline choice only changes speed: both pipelines must be exact on
     # every shape, whatever the sample picked)
     r = subprocess.run([exe, "--pipe=ea", "one", "17", "tiny", "short", "bucket", "near", "small pieces",
-                        "long", "zipf", "verify", "strided"], capture_output=True, text=True, timeout=600)
+                        "long", "zipf", "verify", "strided", "exact fit packed"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "PASS" in r.stdout
+    # verdict r4 item 1: exact-fit batches (every column followed by a guard
+    # page; the r04an shape's first and last workgroups are in the default
+    # run) with every launch forced onto run_lp as well
+    r = subprocess.run([exe, "--pipe=lp", "exact fit packed", "exact fit verify 4 KiB"],
+                       capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "PASS" in r.stdout
 

@@ -648,6 +648,221 @@ def test_balanced_workgroups(engine, oracle, n, lo, hi):
     np.testing.assert_array_equal(m, oracle.batch(buf, offs, lens, inits, mask=True))
 
 
+def _exact_alloc(nbytes):
+    """A device buffer of exactly nbytes (a 2 MiB multiple: the caching
+    allocator rounds large blocks to 2 MiB, so no slack follows the last
+    byte) from a fresh segment."""
+    import torch
+    assert nbytes % (2 << 20) == 0
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+
+
+def test_exact_fit_4k_blocks_2gib(engine, reference):
+    """Verdict r4 item 1 (profiles/r04an_balance.log): the `4k` shape of
+    scripts/balance_ab.py -- 512 Ki aligned 4 KiB blocks filling a 2 GiB
+    buffer to its last byte, offsets / lengths / outputs exactly 4 / 2 / 2
+    MiB -- with HCRC_BALANCE on and off (run_ea), CRC and ReadBlock verify
+    (handle 4091 + type byte + trailer ending at the buffer's end), every CRC
+    against the compiled reference.  The kernel side of the same launch is
+    replayed in the SIMT emulator with guard pages after every column
+    (tests/cpp/test_lp_emu.cc "exact fit")."""
+    import torch
+    n, bs = 1 << 19, 4096
+    dbuf = _exact_alloc(n * bs)
+    engine.fill_splitmix64_device(dbuf, 0xE4AC7)
+    offs = torch.arange(n, dtype=torch.int64, device="cuda:0") * bs
+    lens = torch.full((n,), bs, dtype=torch.int32, device="cuda:0")
+    plain = _u32(engine.batch_device(dbuf, offs, lens))
+    bal = _u32(engine.batch_device(dbuf, offs, lens, balance=True))
+    np.testing.assert_array_equal(plain, bal)
+    host = dbuf.cpu().numpy()
+    want = reference.batch(host, np.arange(n, dtype=np.uint64) * bs, np.full(n, bs, np.uint32),
+                           threads=8)
+    np.testing.assert_array_equal(plain, want)
+    # ReadBlock: block i = 4091 content bytes + type byte + LE32(Mask(crc))
+    crc = engine.batch_device(dbuf, offs, torch.full((n,), bs - 4, dtype=torch.int32,
+                                                     device="cuda:0"), mask_output=True)
+    dbuf.view(torch.int32).view(n, bs // 4)[:, -1] = crc
+    bad = np.random.default_rng(5).choice(n, 97, replace=False)
+    bad = np.union1d(bad, [n - 1])  # the last trailer, at the buffer's last bytes
+    words = dbuf.view(torch.int32).view(n, bs // 4)
+    idx = torch.from_numpy(bad.astype(np.int64)).to("cuda:0")
+    words[idx, -1] = words[idx, -1] ^ 0x10
+    status = engine.verify_device(dbuf, offs, torch.full((n,), bs - 5, dtype=torch.int32,
+                                                         device="cuda:0"))
+    expect = np.ones(n, np.uint8)
+    expect[bad] = 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(status.cpu().numpy(), expect)
+    del dbuf, host
+
+
+@pytest.mark.parametrize("shape", ["tblocks", "short"])
+def test_exact_fit_packed_spans(engine, oracle, shape):
+    """Exact-fit SST-packed batches: the last span ends at the last byte of a
+    2 MiB-multiple device buffer.  Table blocks (run_ea) and 512 B..2 KiB
+    spans (run_lp), HCRC_BALANCE on and off, masked, and ReadBlock verify of
+    the same layout with trailers (the last trailer at the buffer's end),
+    against the oracle."""
+    import torch
+    rng = np.random.default_rng(77 if shape == "tblocks" else 78)
+    total = 64 << 20
+    lo, hi = (4097, 4225) if shape == "tblocks" else (512, 2200)
+    lens = rng.integers(lo, hi + 1, total // lo).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens + 5)[:-1]]).astype(np.uint64)
+    keep = int(np.searchsorted(offs + lens + 5, total - hi - 5, side="right"))
+    offs, lens = offs[:keep + 1], lens[:keep + 1]
+    lens[-1] = total - 5 - int(offs[-1])  # the last block + type + trailer end the buffer
+    lens = lens.astype(np.uint32)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    # CRC spans cover contents + type (+1); verify's handles are contents
+    vlen = lens + 1
+    for i in range(offs.size):
+        c = oracle.extend(0, host, int(offs[i]), int(vlen[i]))
+        host[int(offs[i]) + int(vlen[i]):int(offs[i]) + int(vlen[i]) + 4] = np.frombuffer(
+            int(oracle.lib.oracle_mask(c)).to_bytes(4, "little"), np.uint8)
+    bad = rng.choice(offs.size, 41, replace=False)
+    bad = np.union1d(bad, [offs.size - 1])
+    for b in bad:
+        host[int(offs[b]) + int(vlen[b]) + 3] ^= 0x01  # the trailer's last byte
+    dbuf = _exact_alloc(total)
+    dbuf.copy_(torch.from_numpy(host))
+    d_off, d_len = _t(offs), _t(vlen)
+    # CRC: the last span's last byte is the buffer's last byte
+    d_len_end = _t(np.append(vlen[:-1], vlen[-1] + 4).astype(np.uint32))
+    want = oracle.batch(host, offs, np.append(vlen[:-1], vlen[-1] + 4).astype(np.uint32))
+    for balance in (False, True):
+        got = _u32(engine.batch_device(dbuf, d_off, d_len_end, balance=balance))
+        np.testing.assert_array_equal(got, want)
+        got = _u32(engine.batch_device(dbuf, d_off, d_len_end, mask_output=True, balance=balance))
+        np.testing.assert_array_equal(got, np.array([oracle.lib.oracle_mask(int(x)) for x in want],
+                                                    np.uint32))
+    del d_len
+    status = engine.verify_device(dbuf, d_off, _t(lens))
+    expect = np.ones(offs.size, np.uint8)
+    expect[bad] = 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(status.cpu().numpy(), expect)
+    del dbuf
+
+
+def _packed_layout(rng, n, lo, hi, glo, ghi, start=0, short_every=0):
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint64)
+    if short_every:
+        k = np.arange(n) % short_every == 1
+        lens[k] = rng.integers(0, 64, int(k.sum()))
+    gaps = rng.integers(glo, ghi + 1, n).astype(np.uint64)
+    offs = start + np.concatenate([[0], np.cumsum(lens + gaps)[:-1]]).astype(np.uint64)
+    return offs, lens.astype(np.uint32)
+
+
+@pytest.mark.parametrize("shape", ["512-2k", "tblocks", "aligned4k", "zipf", "ragged", "exact"])
+def test_packed_batches(engine, oracle, shape):
+    """HCRC_PACKED (the stream-tiled kernel, crc32c_ps.h) against the oracle:
+    SST-packed 512 B..2 KiB spans, WriteRawBlock-shaped table blocks (gap 4),
+    contiguous aligned 4 KiB blocks, a Zipf mix, short / empty spans among
+    the stream ones with ragged gaps 0..300 (and 0..3: words shared across a
+    gap), an exact fit at a 2 MiB-multiple buffer's end; with inits and the
+    masked output."""
+    import torch
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(shape.encode()))
+    if shape == "512-2k":
+        offs, lens = _packed_layout(rng, 30000, 512, 2200, 5, 5, 3)
+    elif shape == "tblocks":
+        offs, lens = _packed_layout(rng, 12000, 4097, 4225, 4, 4)
+    elif shape == "aligned4k":
+        offs, lens = np.arange(12000, dtype=np.uint64) * 4096, np.full(12000, 4096, np.uint32)
+    elif shape == "zipf":
+        b = np.array([512, 1024, 2048, 4096, 8192, 16384, 32768, 65536])
+        p = 1.0 / np.arange(1, 9) ** 0.99
+        L = b[rng.choice(8, 6000, p=p / p.sum())]
+        lens = (L + rng.integers(0, L // 8 + 1)).astype(np.uint32)
+        offs = 1 + np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 5)[:-1]]).astype(np.uint64)
+    elif shape == "ragged":
+        o1, l1 = _packed_layout(rng, 12000, 64, 3000, 0, 300, 5, short_every=17)
+        o2, l2 = _packed_layout(rng, 12000, 64, 3000, 0, 3, 2 + int(o1[-1] + l1[-1]), short_every=23)
+        offs, lens = np.concatenate([o1, o2]), np.concatenate([l1, l2])
+    else:  # exact: the last span ends at the buffer's last byte
+        offs, lens = _packed_layout(rng, 9000, 700, 5000, 4, 4)
+    size = int(offs[-1] + lens[-1])
+    if shape == "exact":
+        total = (size + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+        offs = offs + np.uint64(total - size)
+        size = total
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    dbuf = _exact_alloc(size) if shape == "exact" else torch.from_numpy(host).cuda()
+    if shape == "exact":
+        dbuf.copy_(torch.from_numpy(host))
+    inits = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    do, dl, di = _t(offs), _t(lens), _t(inits)
+    want = oracle.batch(host, offs, lens)
+    got = _u32(engine.batch_device(dbuf, do, dl, packed=True))
+    np.testing.assert_array_equal(got, want)
+    got = _u32(engine.batch_device(dbuf, do, dl, di, mask_output=True, packed=True))
+    np.testing.assert_array_equal(got, oracle.batch(host, offs, lens, inits, mask=True))
+    del dbuf
+
+
+def test_packed_promise_broken_falls_back(engine, oracle):
+    """HCRC_PACKED on batches that are NOT packed -- unsorted, overlapping, a
+    5 KiB gap, dense spans of a few bytes -- computes them all the same (the
+    pre-pass sends them to the default pipeline)."""
+    rng = np.random.default_rng(31)
+    offs, lens = _packed_layout(rng, 8000, 300, 3000, 5, 5, 3)
+    cases = []
+    o = offs.copy()
+    o[[100, 101]] = o[[101, 100]]
+    cases.append((o, lens.copy()))
+    o = offs.copy()
+    o[500] -= 10
+    cases.append((o, lens))
+    o = offs.copy()
+    o[700:] += 5000
+    cases.append((o, lens))
+    o4, l4 = _packed_layout(rng, 20000, 5, 60, 7, 7, 1)
+    cases.append((o4, l4))
+    for o, ln in cases:
+        host = rng.integers(0, 256, int(o.max() + ln.max()) + 8, dtype=np.uint8)
+        got = _run_device_packed(engine, host, o, ln)
+        np.testing.assert_array_equal(got, oracle.batch(host, o, ln))
+
+
+def _run_device_packed(engine, buf, offs, lens):
+    out = engine.batch_device(_t(buf), _t(np.asarray(offs, np.uint64)),
+                              _t(np.asarray(lens, np.uint32)), packed=True)
+    return _u32(out)
+
+
+def test_packed_config3_full_size(engine, reference):
+    """Config 3's 2 GiB Zipf mix (SST-packed, gap 5, unaligned) through
+    HCRC_PACKED: every CRC equal to the default pipeline's, and a 64 Ki-span
+    sample against the compiled reference."""
+    import torch
+    rng = np.random.default_rng(33)
+    nbytes = 2 << 30
+    b = np.array([512, 1024, 2048, 4096, 8192, 16384, 32768, 65536])
+    p = 1.0 / np.arange(1, 9) ** 0.99
+    L = b[rng.choice(8, 290000, p=p / p.sum())]
+    lens = (L + rng.integers(0, L // 8 + 1)).astype(np.uint64)
+    offs = 3 + np.concatenate([[0], np.cumsum(lens + 5)[:-1]]).astype(np.uint64)
+    keep = offs + lens <= nbytes
+    offs, lens = offs[keep], lens[keep].astype(np.uint32)
+    dbuf = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    engine.fill_splitmix64_device(dbuf, 0x3C)
+    do, dl = _t(offs), _t(lens)
+    default = engine.batch_device(dbuf, do, dl)
+    packed = engine.batch_device(dbuf, do, dl, packed=True)
+    assert bool((default == packed).all())
+    idx = np.sort(rng.choice(offs.size, 1 << 16, replace=False))
+    host = dbuf.cpu().numpy()
+    want = reference.batch(host, offs[idx], lens[idx], threads=8)
+    np.testing.assert_array_equal(_u32(packed)[idx], want)
+    del dbuf, host
+
+
 def test_full_size_4k_blocks(engine, oracle, reference):
     """BASELINE configs[1]: 1 M x 4 KiB device-resident, device-generated."""
     import torch
@@ -1043,6 +1258,57 @@ def test_kernel_fault_is_reported(tmp_path):
     r = subprocess.run([exe, "4"], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, WIPDB_HCRC_FORCE_FAULT="1"))
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_kernel_fault_stays_with_its_stream():
+    """an async launch's fault is reported to the caller of ITS
+    stream only.  Test build: a launch on stream A with the forced fault, one
+    on stream B without; B is synchronised first and reports nothing, then A
+    reports HCRC_ERR_KERNEL once; a synchronous batch in between (its own
+    lane's word) is unaffected, and a synchronous call's fault is not
+    reported to an async stream afterwards."""
+    assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
+    code = (
+        "import numpy as np, torch\n"
+        "from wipdb_amd import Engine, HcrcError, _lib\n"
+        "lib = _lib.load()\n"
+        "rng = np.random.default_rng(6)\n"
+        "n = 2000\n"
+        "buf = rng.integers(0, 256, n * 1100 + 64, dtype=np.uint8)\n"
+        "lens = rng.integers(1, 1000, n).astype(np.uint32)\n"
+        "offs = (np.arange(n, dtype=np.uint64) * 1100)\n"
+        "def rc_of(f):\n"
+        "    try:\n"
+        "        f()\n"
+        "        return 0\n"
+        "    except HcrcError as e:\n"
+        "        return e.code\n"
+        "with Engine(0) as eng:\n"
+        "    d = torch.from_numpy(buf).cuda()\n"
+        "    do = torch.from_numpy(offs.view(np.int64)).cuda()\n"
+        "    dl = torch.from_numpy(lens.view(np.int32)).cuda()\n"
+        "    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()\n"
+        "    torch.cuda.synchronize()\n"
+        "    lib.hcrc_test_force_fault(1)\n"
+        "    eng.batch_device(d, do, dl, stream=sa.cuda_stream)\n"
+        "    lib.hcrc_test_force_fault(0)\n"
+        "    eng.batch_device(d, do, dl, stream=sb.cuda_stream)\n"
+        "    assert rc_of(lambda: eng.sync(sb.cuda_stream)) == 0\n"
+        "    assert rc_of(lambda: eng.batch(buf, offs, lens)) == 0\n"
+        "    assert rc_of(lambda: eng.sync(sa.cuda_stream)) == _lib.HCRC_ERR_KERNEL\n"
+        "    assert rc_of(lambda: eng.sync(sa.cuda_stream)) == 0  # reported once\n"
+        "    lib.hcrc_test_force_fault(1)\n"
+        "    assert rc_of(lambda: eng.batch(buf, offs, lens)) == _lib.HCRC_ERR_KERNEL\n"
+        "    lib.hcrc_test_force_fault(0)\n"
+        "    eng.batch_device(d, do, dl, stream=sb.cuda_stream)\n"
+        "    assert rc_of(lambda: eng.sync(sb.cuda_stream)) == 0\n"
+        "    assert lib.hcrc_ctx_check(eng._ctx) == _lib.HCRC_OK\n"
+        "print('stream faults ok')\n")
+    env = dict(os.environ, PYTHONPATH=REPO, WIPDB_HCRC_LIB=TEST_LIB)
+    env.pop("WIPDB_HCRC_FORCE_FAULT", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "stream faults ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
 
 
 def test_no_fault_in_healthy_launches(engine):

@@ -357,31 +357,90 @@ LEVELDB_ADAPTER_PREBUILT = os.path.join(REPO, "oracle", "_ref", "test_leveldb_ad
 
 
 @pytest.fixture(scope="module")
-def leveldb_adapter(tmp_path_factory):
-    """tests/cpp/test_leveldb_adapter.cc built against leveldb's public headers
-    (header-only: no leveldb source is compiled) and this library."""
-    if not os.path.isdir(LEVELDB_INCLUDE):
-        # the GPU box: the copy oracle/Makefile built where the reference was
-        if os.path.exists(LEVELDB_ADAPTER_PREBUILT):
-            return LEVELDB_ADAPTER_PREBUILT
-        pytest.skip("leveldb headers absent (the reference tree is not on this machine)")
-    exe = str(tmp_path_factory.mktemp("ldb") / "test_leveldb_adapter")
-    libdir = os.path.join(REPO, "wipdb_amd", "lib")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"), "-I",
-                    LEVELDB_INCLUDE, os.path.join(REPO, "tests", "cpp", "test_leveldb_adapter.cc"),
-                    "-L", libdir, "-lhip_crc32c_batch", f"-Wl,-rpath,{libdir}", "-o", exe],
-                   check=True)
-    return exe
+def leveldb_adapter():
+    """tests/cpp/test_leveldb_adapter.cc, built by oracle/Makefile against
+    leveldb's headers, leveldb's table code compiled in place (its real
+    comparators and bloom filter) and this library."""
+    if not os.path.exists(LEVELDB_ADAPTER_PREBUILT):
+        pytest.skip("oracle/_ref/test_leveldb_adapter not built (reference absent, no prebuilt copy)")
+    return LEVELDB_ADAPTER_PREBUILT
 
 
 LEVELDB_CONFIGS = [("8binsert", 3000, 4096, 16, 10, False), ("mixed", 1500, 1024, 4, 0, False),
                    ("internal", 2500, 4096, 16, 10, True), ("internal", 800, 256, 1, 7, True)]
+
+# leveldb's own table code compiled in place (oracle/Makefile LDB_SO; VERDICT
+# r4 item 5), and the same sources with util/crc32c.cc left out, linked to
+# this library's leveldb::crc32c::Extend (LDB_DROPIN_SO)
+REF_LEVELDB_SO = os.path.join(REPO, "oracle", "_ref", "libref_leveldb.so")
+REF_LEVELDB_DROPIN_SO = os.path.join(REPO, "oracle", "_ref", "libref_leveldb_dropin.so")
+
+
+class RefLevelDB:
+    """ctypes view of oracle/_ref/libref_leveldb*.so: leveldb::TableBuilder
+    (leveldb/table/table_builder.cc:185-187), Table::Open + a verified
+    iteration, ReadBlock (format.cc:91-92).  Test infrastructure."""
+
+    def __init__(self, path):
+        lib = ctypes.CDLL(path)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        lib.ldb_build_table_ex.restype = ctypes.c_long
+        lib.ldb_build_table_ex.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, vp, sz]
+        lib.ldb_verify_table.restype = ctypes.c_int
+        lib.ldb_verify_table.argtypes = [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(sz)]
+        lib.ldb_read_block.restype = ctypes.c_int
+        lib.ldb_read_block.argtypes = [vp, sz, ctypes.c_uint64, ctypes.c_uint64]
+        lib.ldb_crc32c_value.restype = ctypes.c_uint32
+        lib.ldb_crc32c_value.argtypes = [ctypes.c_char_p, sz]
+        self.lib = lib
+
+    def build(self, kvs, block_size=4096, restart=16, bloom=0, internal=False) -> bytes:
+        keys = b"".join(k for k, _ in kvs)
+        vals = b"".join(v for _, v in kvs)
+        kl = np.array([len(k) for k, _ in kvs] or [0], np.uint32)
+        vl = np.array([len(v) for _, v in kvs] or [0], np.uint32)
+        cap = 2 * (len(keys) + len(vals)) + 8192 + 64 * len(kvs)
+        out = ctypes.create_string_buffer(cap)
+        kb = ctypes.create_string_buffer(keys, len(keys) or 1)
+        vb = ctypes.create_string_buffer(vals, len(vals) or 1)
+        n = self.lib.ldb_build_table_ex(kb, kl.ctypes.data, vb, vl.ctypes.data, len(kvs),
+                                        block_size, restart, bloom, int(internal), out, cap)
+        assert 0 < n <= cap
+        return out.raw[:n]
+
+    def verify(self, img: bytes, bloom=0, internal=False) -> int:
+        b = ctypes.create_string_buffer(img, len(img) or 1)
+        nb = ctypes.c_size_t(0)
+        return int(self.lib.ldb_verify_table(b, len(img), bloom, int(internal), ctypes.byref(nb)))
+
+    def read_block(self, img: bytes, off: int, size: int) -> int:
+        b = ctypes.create_string_buffer(img, len(img) or 1)
+        return int(self.lib.ldb_read_block(b, len(img), off, size))
+
+
+@pytest.fixture(scope="module", params=["leveldb", "leveldb-dropin"])
+def ref_leveldb(request):
+    path = REF_LEVELDB_SO if request.param == "leveldb" else REF_LEVELDB_DROPIN_SO
+    if not os.path.exists(path):
+        pytest.skip(f"{os.path.relpath(path, REPO)} not built (reference absent, no prebuilt copy)")
+    return RefLevelDB(path)
+
+
+def test_leveldb_reference_kat(ref_leveldb):
+    """leveldb's crc32c compiled in place (and the product's, in the drop-in
+    build) on the leveldb KAT (leveldb/util/crc32c_test.cc)."""
+    assert ref_leveldb.lib.ldb_crc32c_value(b"123456789", 9) == 0xE3069283
 
 
 @pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
 @pytest.mark.parametrize("cfg", LEVELDB_CONFIGS, ids=[f"{c[0]}-b{c[2]}-r{c[3]}-f{c[4]}"
                                                        for c in LEVELDB_CONFIGS])
 def test_leveldb_adapter_bytes_equal_reference(ref_table, leveldb_adapter, tmp_path, cfg, mode):
+    _adapter_table(ref_table, leveldb_adapter, tmp_path, cfg, mode)
+
+
+def _adapter_table(ref_table, leveldb_adapter, tmp_path, cfg, mode):
     """The leveldb/table call sites (leveldb/table/table_builder.cc:185-187
     write side, format.cc:91-92 read side) through the adapter: a table
     written with WritableFileSink + TableOptionsFrom(leveldb::Options-shaped
@@ -400,9 +459,50 @@ def test_leveldb_adapter_bytes_equal_reference(ref_table, leveldb_adapter, tmp_p
                         str(int(internal)), str(mode)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     got = out.read_bytes()
-    assert got == ref_table.build(kvs, block_size=bs, restart=restart, bloom=bloom,
-                                  internal=internal)
+    # kv's reader accepts it (the framing is kv's; the index separators are
+    # leveldb's comparator's, so the bytes are leveldb's, not kv's builder's)
     assert ref_table.verify(got, bloom) == 0
+    return got, kvs
+
+
+@pytest.mark.parametrize("mode", [sst.CRC_INLINE, sst.CRC_BATCH_CPU])
+@pytest.mark.parametrize("cfg", LEVELDB_CONFIGS, ids=[f"{c[0]}-b{c[2]}-r{c[3]}-f{c[4]}"
+                                                       for c in LEVELDB_CONFIGS])
+def test_leveldb_adapter_bytes_equal_leveldb_builder(ref_table, ref_leveldb, leveldb_adapter,
+                                                     tmp_path, cfg, mode):
+    """the adapter's table equals the file leveldb's OWN
+    TableBuilder writes (leveldb/table/table_builder.cc:185-187, compiled in
+    place, and again with its crc32c taken from this library), and leveldb's
+    Table::Open + verified iteration accepts it."""
+    got, kvs = _adapter_table(ref_table, leveldb_adapter, tmp_path, cfg, mode)
+    kind, n, bs, restart, bloom, internal = cfg
+    assert got == ref_leveldb.build(kvs, block_size=bs, restart=restart, bloom=bloom,
+                                    internal=internal)
+    assert ref_leveldb.verify(got, bloom, internal) == 0
+
+
+def test_read_block_statuses_match_leveldb(ref_leveldb):
+    """ReadBlock's verdicts (leveldb/table/format.cc:91-92) on every block of
+    a leveldb-built table, clean and with seeded damage in the contents, the
+    type byte and the trailer: the library's read_block (batched CRC path)
+    returns leveldb's status for each."""
+    kvs = kv_8binsert(4000, 23)
+    img = ref_leveldb.build(kvs, bloom=10)
+    rng = np.random.default_rng(24)
+    for o, s in _handles(img):
+        assert sst.read_block(img, o, s) == ref_leveldb.read_block(img, o, s) == sst.OK
+        for where in (int(rng.integers(0, s)), s, s + 1, s + 4):  # contents, type, trailer
+            b = bytearray(img)
+            b[o + where] ^= 1 << int(rng.integers(0, 8))
+            assert sst.read_block(bytes(b), o, s) == ref_leveldb.read_block(bytes(b), o, s)
+    assert ref_leveldb.verify(img, 10) == 0
+    # whole-table verification over seeded corruptions: the same verdicts
+    for case in range(30):
+        b = bytearray(img)
+        b[int(rng.integers(0, len(b) - 48))] ^= 1 << int(rng.integers(0, 8))
+        want = ref_leveldb.verify(bytes(b), 10)
+        rc, codes = sst.verify_tables([bytes(b)], 10, sst.CRC_BATCH_CPU)
+        assert codes[0] == want, case
 
 
 # ---- the compaction input path (MakeInputIteratorKV) -----------------------
@@ -646,15 +746,18 @@ def test_gpu_table_bytes_equal_reference(ref_table, cfg, engine):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", LEVELDB_CONFIGS, ids=[f"{c[0]}-b{c[2]}-r{c[3]}-f{c[4]}"
                                                        for c in LEVELDB_CONFIGS])
-def test_gpu_leveldb_adapter_bytes_equal_reference(ref_table, leveldb_adapter, tmp_path, cfg,
-                                                   engine):
-    """the leveldb/table call sites through the adapter
-    (leveldb/table/table_builder.cc:185-187, format.cc:91-92) with the block
-    CRCs batched on the MI355X (CRC_BATCH_GPU, write and verify side): the
-    same bytes as the reference's kv::TableBuilder (leveldb's own builder is
-    not compiled here: parity-unpinned beyond that kv equivalence)."""
-    test_leveldb_adapter_bytes_equal_reference(ref_table, leveldb_adapter, tmp_path, cfg,
-                                               sst.CRC_BATCH_GPU)
+def test_gpu_leveldb_adapter_bytes_equal_reference(ref_table, ref_leveldb, leveldb_adapter,
+                                                   tmp_path, cfg, engine):
+    """The leveldb/table call sites through the adapter (leveldb/table/
+    table_builder.cc:185-187, format.cc:91-92) with the block CRCs batched on
+    the MI355X (CRC_BATCH_GPU, write and verify side): the same bytes as the
+    reference's kv::TableBuilder and as leveldb's own TableBuilder (compiled
+    in place, and with its crc32c from this library), which accepts them."""
+    got, kvs = _adapter_table(ref_table, leveldb_adapter, tmp_path, cfg, sst.CRC_BATCH_GPU)
+    kind, n, bs, restart, bloom, internal = cfg
+    assert got == ref_leveldb.build(kvs, block_size=bs, restart=restart, bloom=bloom,
+                                    internal=internal)
+    assert ref_leveldb.verify(got, bloom, internal) == 0
 
 
 @pytest.mark.gpu

@@ -33,6 +33,7 @@ HCRC_MASK_OUTPUT = 0x2
 HCRC_SPLIT_SMALL = 0x4
 HCRC_SPLIT_LONG = 0x8
 HCRC_BALANCE = 0x10
+HCRC_PACKED = 0x20
 
 _c = ctypes
 _u32p = _c.POINTER(_c.c_uint32)

@@ -19,7 +19,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (HCRC_BALANCE, HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HCRC_SPLIT_LONG,
+from ._lib import (HCRC_BALANCE, HCRC_DEVICE_PTRS, HCRC_MASK_OUTPUT, HCRC_PACKED, HCRC_SPLIT_LONG,
                    HCRC_SPLIT_SMALL, HcrcError, check)
 
 MASK_DELTA = 0xA282EAD8
@@ -194,13 +194,16 @@ class Engine:
     def batch_device(self, base_t, offsets_t, lengths_t, inits_t=None, out_t=None,
                      mask_output: bool = False, stream=None, split_small: bool = False,
                      check_bounds: bool = False, split_long: bool = False,
-                     balance: bool = False):
+                     balance: bool = False, packed: bool = False):
         """Asynchronous batch on device tensors; returns the uint32 out tensor
         (int32 storage).  Enqueued on ``stream`` (default: torch's current).
         ``split_small``: HCRC_SPLIT_SMALL (the size classes); ``split_long``:
         HCRC_SPLIT_LONG (spans of >= 128 KiB in 16 KiB parts on many waves;
         batches of at most 16 spans take it by themselves); ``balance``:
-        HCRC_BALANCE (byte-balanced workgroup ranges for mixed sizes).  Offsets are
+        HCRC_BALANCE (byte-balanced workgroup ranges for mixed sizes); ``packed``:
+        HCRC_PACKED (an SST-packed batch -- sorted, no overlap, gaps < 4 KiB --
+        read as one byte stream; checked on the device, a batch that is not
+        packed runs the default pipeline).  Offsets are
         int64, lengths / inits / out 32-bit, all contiguous on this engine's
         device; ``check_bounds`` also checks every span against base (a
         device kernel and a sync, hcrc_check_spans)."""
@@ -216,6 +219,8 @@ class Engine:
             flags |= HCRC_SPLIT_LONG
         if balance:
             flags |= HCRC_BALANCE
+        if packed:
+            flags |= HCRC_PACKED
         check(self._lib.hcrc_batch_async(self._ctx, _ptr(base_t), _ptr(offsets_t), _ptr(lengths_t),
                                          _ptr(inits_t), _ptr(out_t), n, flags,
                                          self._stream_of(stream)), "hcrc_batch_async")
@@ -267,7 +272,7 @@ class Engine:
         import torch
         n = self._check_spans(base_t, offsets_t, lengths_t, None, check_bounds, 5, stream)
         if status_t is None:
-            status_t = torch.empty(n, dtype=torch.uint8, device=base_t.device)
+            status_t = torch.zeros(n, dtype=torch.uint8, device=base_t.device)
         _check_tensor(status_t, "status", self._device(), _dtypes()[2], n)
         check(self._lib.hcrc_verify_async_ex(self._ctx, _ptr(base_t), _ptr(offsets_t),
                                              _ptr(lengths_t), _ptr(status_t), n,
@@ -295,7 +300,11 @@ class Engine:
         return dst_t
 
     def sync(self, stream=None) -> None:
-        check(self._lib.hcrc_sync(self._ctx, stream or 0), "hcrc_sync")
+        """hcrc_sync on ``stream`` (default: torch's current stream, as the
+        async entry points): waits for it, then raises HCRC_ERR_KERNEL if one
+        of this context's launches on that stream reported an in-kernel
+        fault since the stream's last check."""
+        check(self._lib.hcrc_sync(self._ctx, self._stream_of(stream)), "hcrc_sync")
 
 
 def batch_multi(devices: Sequence[int], base, offsets, lengths, inits=None,

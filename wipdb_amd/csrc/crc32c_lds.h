@@ -76,6 +76,7 @@ constexpr uint32_t kMiscIdle = 276;    // waves out of work, waiting for shared 
 constexpr uint32_t kMiscHeld = 277;    // long spans held by a wave, not taken or shared yet
 constexpr uint32_t kMiscQRes = 278;    // queue records pushed and not yet freed (<= kQSlots)
 constexpr uint32_t kMiscFault = 279;   // kFault* bits of the workgroup (run_lp)
+constexpr uint32_t kMiscFaultWord = 280;  // 2 words: the launch's fault word (run_lp)
 constexpr uint32_t kMiscQInit = 576;   // 256 words: the init_crc of queue record k
 constexpr uint32_t kMiscBytes = 1024 * 4;
 
@@ -100,6 +101,16 @@ constexpr uint32_t kFlagMask = 0x2;
 // wrote it, a queue slot never freed for its next record.
 constexpr uint32_t kFaultQueuePop = 0x1;
 constexpr uint32_t kFaultQueueSlot = 0x2;
+// run_ps: a desk that could not advance (never in a batch its pre-pass
+// passed: at most 63 spans meet a window)
+constexpr uint32_t kFaultPsDesk = 0x4;
+
+// HCRC_PACKED (crc32c_ps.h): the meta words of a packed launch (device,
+// zeroed by the host, written by the pre-pass): [0] nonzero = the batch is
+// not packed (kPsBad* bits); [1..2] chunk bytes (u64); [3..4] the first
+// span's start offset (u64).  The chunk index first[C + 1] follows them.
+constexpr uint32_t kPsMetaWords = 8;
+constexpr uint32_t kPsBad = 1u, kPsBadDense = 2u;
 
 // Size classes (HCRC_SPLIT_SMALL).  A span of n bytes at address a covers
 // f = (a % 16 + n) / 16 full chunks of its 16-byte grid.  Class 4 (16-lane

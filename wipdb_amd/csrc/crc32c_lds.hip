@@ -214,15 +214,15 @@ struct SegW {
 constexpr uint32_t kWNone = 0u, kWSeg = 1u, kWBatch = 2u;
 
 #if !defined(WIPDB_LK_EMU)
-// Launches of the lane-packed kernels that reported a fault (kFault*), per
-// device, ever: the host compares it before and after its launches
-// (hcrc_api.cc; wipdb_lp_fault_counter).  A module global rather than a
-// kernel argument: its address is rematerialised where the report is made,
-// so no register stays live for it through the loop.
-__device__ unsigned int g_lp_faults;
-__device__ __forceinline__ void report_fault(uint32_t) {
-  // every lane of the wave adds: the count only needs to grow
-  __hip_atomic_fetch_add(&g_lp_faults, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// A launch that saw a fault (kFault*) sets its own fault word: a word of the
+// context's pinned fault table, one per synchronous lane and one per caller
+// stream (hcrc_api.cc), so a fault is reported to the caller whose launch it
+// was.  The pointer is a kernel argument that run_lp parks in LDS right after
+// the table image (kMiscFaultWord) and reads back only on the way out: no
+// register stays live for it through the loop.  A plain store of 1, system
+// scope (the word is in host memory the host reads after the stream).
+__device__ __forceinline__ void report_fault(unsigned int* word, uint32_t) {
+  if ((lane_tid() & 63u) == 0u) __hip_atomic_store(word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 #endif
 
@@ -240,7 +240,7 @@ __device__ unsigned long long g_lp_prof[4096 * kProfN];
 
 template <int OUT, typename Src>
 __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags,
-                                       const uint8_t* image) {
+                                       const uint8_t* image, unsigned int* fault) {
   constexpr bool kV = OUT == 1;
   const uint32_t l = lane_tid() & 63u;
   const uint32_t w = uni(lane_tid() >> 6);
@@ -248,6 +248,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   const WgUnits units = wg_units(count, src_bounds(src));
   if (units.count == 0u) return;  // no unit of work
   load_image(image, w, l);
+  {  // (every lane of every wave: the same value; each wave reads back its own)
+    const uint64_t fw = reinterpret_cast<uint64_t>(fault);
+    lds_st_sync(MiscAddr(kMiscFaultWord), static_cast<uint32_t>(fw));
+    lds_st_sync(MiscAddr(kMiscFaultWord + 1u), static_cast<uint32_t>(fw >> 32));
+  }
   const Lane lk = make_lane<1>(l);
   Pipe pp;
   pp.init(l, w);
@@ -428,7 +433,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
       lk_sleep();
     }
     // a slot still not freed within the bound is never overwritten: its span
-    // is lost (the record's popper then reports it too) and the launch says so
+    // is lost, and the popper that takes slot qk next finds the OLD record
+    // there (its marker still set) and runs that span a second time -- a
+    // duplicate as well as a loss.  Both are covered by the fault: the launch
+    // says so (kFaultQueueSlot, the launch's fault word), and its outputs are
+    // not to be used (HCRC_ERR_KERNEL)
     if (busy) lds_st_sync(MiscAddr(kMiscFault), kFaultQueueSlot);
     if (lng && !busy) {
       lds_st_sync(ra, static_cast<uint32_t>(a));
@@ -972,7 +981,11 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   // values there; a register for it cost SGPR spills)
   {
     const uint32_t f = uni(lds_ld_sync(MiscAddr(kMiscFault)));
-    if (f != 0u) report_fault(f);
+    if (f != 0u) {
+      const uint64_t fw = (static_cast<uint64_t>(uni(lds_ld_sync(MiscAddr(kMiscFaultWord + 1u)))) << 32) |
+                          uni(lds_ld_sync(MiscAddr(kMiscFaultWord)));
+      report_fault(reinterpret_cast<unsigned int*>(fw), f);
+    }
   }
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
   LP_T(t_end);
@@ -984,6 +997,15 @@ __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags
   }
 #endif
 }
+
+}  // namespace lk
+}  // namespace wipdb
+
+// run_ps, the stream-tiled pipeline of packed batches (HCRC_PACKED)
+#include "crc32c_ps.h"
+
+namespace wipdb {
+namespace lk {
 
 // ---------------------------------------------------------------------------
 // The pipeline of a launch.  run_lp packs short spans (3.3-3.7 TiB/s on the
@@ -1024,27 +1046,64 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_spans_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image,
-    const uint32_t* __restrict__ bounds) {
+    const uint32_t* __restrict__ bounds, unsigned int* fault) {
   const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u, bounds};
   if (pick_ea<false>(src)) run_ea<0>(src, out, flags, image);
-  else run_lp<0>(src, out, flags, image);
+  else run_lp<0>(src, out, flags, image, fault);
 }
 template __global__ void crc32c_lds_spans_kernel<0>(const uint8_t*, const uint64_t*,
                                                     const uint32_t*, const uint32_t*, uint32_t*,
                                                     uint64_t, uint32_t, const uint8_t*,
-                                                    const uint32_t*);
+                                                    const uint32_t*, unsigned int*);
 template __global__ void crc32c_lds_spans_kernel<1>(const uint8_t*, const uint64_t*,
                                                     const uint32_t*, const uint32_t*, uint32_t*,
                                                     uint64_t, uint32_t, const uint8_t*,
-                                                    const uint32_t*);
+                                                    const uint32_t*, unsigned int*);
+
+// Packed batch (HCRC_PACKED, crc32c_ps.h): run_ps when the pre-pass found the
+// batch packed (meta[0] == 0), else the lane-packed pipeline -- a broken
+// promise costs speed, never a CRC.  first / C: the chunk index.
+template <int INIT>
+__global__ __launch_bounds__(kThreads) void crc32c_lds_packed_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
+    const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
+    uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image,
+    const uint32_t* __restrict__ first, const uint32_t* __restrict__ meta, uint32_t C,
+    unsigned int* fault) {
+  const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u, nullptr};
+  if (meta[0] != 0u) run_lp<0>(src, out, flags, image, fault);
+  else run_ps(src, out, flags, image, first, C, fault);
+}
+template __global__ void crc32c_lds_packed_kernel<0>(const uint8_t*, const uint64_t*,
+                                                     const uint32_t*, const uint32_t*, uint32_t*,
+                                                     uint64_t, uint32_t, const uint8_t*,
+                                                     const uint32_t*, const uint32_t*, uint32_t,
+                                                     unsigned int*);
+template __global__ void crc32c_lds_packed_kernel<1>(const uint8_t*, const uint64_t*,
+                                                     const uint32_t*, const uint32_t*, uint32_t*,
+                                                     uint64_t, uint32_t, const uint8_t*,
+                                                     const uint32_t*, const uint32_t*, uint32_t,
+                                                     unsigned int*);
+
+// The packed batch's pre-pass (crc32c_ps.h ps_index): meta zeroed by the host.
+__global__ __launch_bounds__(256) void crc32c_ps_index_kernel(const uint64_t* __restrict__ offsets,
+                                                              const uint32_t* __restrict__ lengths,
+                                                              uint64_t count, uint32_t C,
+                                                              uint32_t* __restrict__ first,
+                                                              uint32_t* __restrict__ meta) {
+  const uint64_t nt = static_cast<uint64_t>(group_count()) * 256u;
+  const uint64_t tid = static_cast<uint64_t>(group_id()) * 256u + (lane_tid() & 255u);
+  ps_index(nullptr, offsets, lengths, count, C, first, meta, tid, nt);
+}
 
 // Fixed-size blocks at a fixed stride.
 __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t length, uint32_t init,
-    uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image) {
+    uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image,
+    unsigned int* fault) {
   const StridedSrc src{base, stride, length, init, count};
   if (pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
-  else run_lp<0>(src, out, flags & kFlagMask, image);
+  else run_lp<0>(src, out, flags & kFlagMask, image, fault);
 }
 
 // Read-side verify (ReadBlock, kv/src/table/format.cc:91-99): block i =
@@ -1053,32 +1112,21 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
 __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, uint8_t* __restrict__ status, uint64_t count,
-    const uint8_t* __restrict__ image) {
+    const uint8_t* __restrict__ image, unsigned int* fault) {
   const DescSrc<false> src{base, offsets, lengths, nullptr, count, 1u, nullptr};
   if (pick_ea<true>(src)) run_ea<1>(src, status, 0u, image);
-  else run_lp<1>(src, status, 0u, image);
+  else run_lp<1>(src, status, 0u, image, fault);
 }
 
 }  // namespace lk
 }  // namespace wipdb
 
 #if !defined(WIPDB_LK_EMU)
-// Counts one fault as a faulting wave does (the test build's
+// Sets a launch's fault word as a faulting wave does (the test build's
 // WIPDB_HCRC_FORCE_FAULT launches it after each lane-packed launch).
-__global__ void crc32c_lds_fault_probe_kernel() {
-  if (threadIdx.x == 0) wipdb::lk::report_fault(wipdb::lk::kFaultQueuePop);
+__global__ void crc32c_lds_fault_probe_kernel(unsigned int* fault) {
+  if (threadIdx.x == 0) wipdb::lk::report_fault(fault, wipdb::lk::kFaultQueuePop);
 }
-
-// The device address of g_lp_faults on the current device (hcrc_api.cc).
-namespace wipdb {
-namespace lk {
-unsigned int* LpFaultCounter() {
-  void* p = nullptr;
-  return hipGetSymbolAddress(&p, HIP_SYMBOL(g_lp_faults)) == hipSuccess
-             ? static_cast<unsigned int*>(p) : nullptr;
-}
-}  // namespace lk
-}  // namespace wipdb
 #endif
 
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)

@@ -47,6 +47,10 @@ __device__ __forceinline__ void lds_st_sync(uint32_t a, uint32_t v) {
 // every LDS access of this wave has completed (and none moves across)
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void compiler_barrier() { asm volatile("" ::: "memory"); }
+// LDS writes of some lanes, then reads of the same words by other lanes of
+// the wave: the wave's DS instructions execute in order, so program order is
+// enough here (the host emulation, a thread per lane, meets at a barrier)
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // v was loaded from global memory and that load is known to be complete
 // (a wait on the DMA issued after it): an asm use makes the compiler place
 // its own wait for the load here, where it costs nothing, and not at a later
@@ -57,6 +61,11 @@ __device__ __forceinline__ void loads_landed(T& v) { asm volatile("" : "+v"(v));
 // a vector load (its wait is a vmcnt one, ordered with the DMA, not an lgkmcnt
 // one that every later LDS access would also wait for)
 __device__ __forceinline__ uint32_t vzero() { return __builtin_amdgcn_mbcnt_lo(0u, 0u); }
+
+// a |= v in global memory (agent scope; the pre-pass's verdict word)
+__device__ __forceinline__ void global_or(uint32_t* a, uint32_t v) {
+  __hip_atomic_fetch_or(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---- faults ----
 // A queue record's marker as read (the host emulation can hide one to force

@@ -38,12 +38,19 @@ namespace lk {
 template <int INIT>
 __global__ void crc32c_lds_spans_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                         const uint32_t*, uint32_t*, uint64_t, uint32_t,
-                                        const uint8_t*, const uint32_t*);
+                                        const uint8_t*, const uint32_t*, unsigned int*);
 __global__ void crc32c_lds_strided_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t,
-                                          uint32_t*, uint64_t, uint32_t, const uint8_t*);
+                                          uint32_t*, uint64_t, uint32_t, const uint8_t*,
+                                          unsigned int*);
 __global__ void crc32c_lds_verify_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
-                                         uint8_t*, uint64_t, const uint8_t*);
-unsigned int* LpFaultCounter();
+                                         uint8_t*, uint64_t, const uint8_t*, unsigned int*);
+template <int INIT>
+__global__ void crc32c_lds_packed_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
+                                         const uint32_t*, uint32_t*, uint64_t, uint32_t,
+                                         const uint8_t*, const uint32_t*, const uint32_t*, uint32_t,
+                                         unsigned int*);
+__global__ void crc32c_ps_index_kernel(const uint64_t*, const uint32_t*, uint64_t, uint32_t,
+                                       uint32_t*, uint32_t*);
 template <int G, int OUT>
 __global__ void crc32c_lds_list_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                        const uint32_t*, const uint32_t*, const uint32_t*, void*,
@@ -70,7 +77,7 @@ __global__ void split_combine_kernel(const uint32_t*, const uint32_t*, const uin
 }  // namespace util
 }  // namespace wipdb
 
-__global__ void crc32c_lds_fault_probe_kernel();
+__global__ void crc32c_lds_fault_probe_kernel(unsigned int*);
 
 namespace lk = wipdb::lk;
 
@@ -112,6 +119,12 @@ class DeviceGuard {
 constexpr size_t kStageBytes = size_t(32) << 20;  // pinned staging per slot
 constexpr size_t kStageSpans = size_t(1) << 17;   // descriptors per slot
 constexpr int kMaxLanes = 8;                      // concurrent synchronous calls per context
+// Fault words of the lane-packed kernels (crc32c_lds.hip report_fault): one
+// per launch owner -- word k (1 .. kMaxLanes) for synchronous lane k, then
+// one per caller stream of the *_async entry points (kStreamFaultWords; past
+// that, streams share word 0).
+constexpr uint32_t kStreamFaultWords = 1024;
+constexpr uint32_t kFaultWords = 1 + kMaxLanes + kStreamFaultWords;
 
 // One piece of a host batch in flight: pinned host buffers and their device
 // mirrors.
@@ -208,7 +221,7 @@ struct Lane {
   hipStream_t stream = nullptr;
   Slot slots[2];
   bool slots_ready = false;
-  int index = 0;  // its fault snapshots: hcrc_ctx::h_faults[2 index ..] (1 .. kMaxLanes)
+  int index = 0;  // 1 .. kMaxLanes: its fault word (hcrc_ctx::fault_words[index])
 };
 
 // Host ranges pinned (hcrc_host_alloc) or registered (hcrc_host_register)
@@ -265,18 +278,24 @@ struct hcrc_ctx {
   // stream-ordered scratch (size-class lists) from a private pool that keeps
   // its memory mapped between calls (release threshold: never)
   hipMemPool_t scratch_pool = nullptr;
-  // faults of the lane-packed kernels (crc32c_lds.h kFault*): the device's
-  // count of faulting waves (a module global, only ever grows), pinned
-  // snapshots of it (lane k: [2k] before its launches, [2k + 1] after), and
-  // the count hcrc_ctx_check last saw (launches on callers' streams)
-  const unsigned int* d_faults = nullptr;
-  unsigned int* h_faults = nullptr;
-  std::atomic<unsigned int> faults_seen{0};
+  // fault words of the lane-packed kernels (kFaultWords, pinned coherent
+  // host memory the kernels write with a system-scope store; d_: its device
+  // view): a launch that saw a fault (crc32c_lds.h kFault*) sets its owner's
+  // word, so the fault is reported to that owner only -- a synchronous
+  // call's lane, or the caller stream of an async launch (stream_words,
+  // assigned on first use; hcrc_sync / hcrc_ctx_check read and clear them)
+  unsigned int* fault_words = nullptr;
+  unsigned int* d_fault_words = nullptr;
+  std::mutex faults_mu;
+  std::map<hipStream_t, uint32_t> stream_words;
   // lanes of synchronous calls
   std::mutex lanes_mu;
   std::condition_variable lanes_cv;
   std::vector<Lane*> free_lanes;
   std::vector<std::unique_ptr<Lane>> lanes;
+  // Releases what the context holds: hcrc_ctx_destroy, and every error
+  // return of hcrc_ctx_create after a partial construction.
+  ~hcrc_ctx();
 };
 
 namespace {
@@ -328,20 +347,20 @@ class LaneLease {
     if (!lane_->stream) HCRC_CHECK(hipStreamCreateWithFlags(&lane_->stream, hipStreamNonBlocking));
     return HCRC_OK;
   }
-  // The device's fault count before the call's launches (stream order).
+  // The lane's fault word, cleared before the call's launches (the lane's
+  // earlier launches are complete: its calls are synchronous).
   int FaultsBefore() {
-    HCRC_CHECK(hipMemcpyAsync(ctx_->h_faults + 2 * lane_->index, ctx_->d_faults, 4,
-                              hipMemcpyDeviceToHost, lane_->stream));
+    __atomic_store_n(ctx_->fault_words + lane_->index, 0u, __ATOMIC_SEQ_CST);
     return HCRC_OK;
   }
-  // After the call's launches: HCRC_ERR_KERNEL if the count grew (one of
-  // them -- or, conservatively, a concurrent call's -- left a span
-  // uncomputed), else HCRC_OK.  Waits for the stream.
+  // The device view of the lane's fault word (the kernels' argument).
+  unsigned int* FaultWord() const { return ctx_->d_fault_words + lane_->index; }
+  // After the call's launches: waits for the stream, then HCRC_ERR_KERNEL if
+  // one of them left a span uncomputed, else HCRC_OK.
   int CheckFaults() {
-    unsigned int* h = ctx_->h_faults + 2 * lane_->index;
-    HCRC_CHECK(hipMemcpyAsync(h + 1, ctx_->d_faults, 4, hipMemcpyDeviceToHost, lane_->stream));
     HCRC_CHECK(hipStreamSynchronize(lane_->stream));
-    return h[1] != h[0] ? HCRC_ERR_KERNEL : HCRC_OK;
+    return __atomic_load_n(ctx_->fault_words + lane_->index, __ATOMIC_SEQ_CST) ? HCRC_ERR_KERNEL
+                                                                                : HCRC_OK;
   }
   // Stream and staging slots.
   int Staging() {
@@ -504,28 +523,46 @@ enum class AutoLong { kNo, kDevice };
 // Test build only (make testlib, tests/test_gpu_parity.py): with
 // WIPDB_HCRC_FORCE_FAULT=1 every lane-packed launch reports a fault (its
 // error word set after it, as the kernel would) -- the HCRC_ERR_KERNEL paths.
+// hcrc_test_force_fault(on) overrides it from then on (per-stream tests).
+std::atomic<int> g_force_fault{-1};
 bool ForcedFault() {
-  static const bool on = [] {
+  int f = g_force_fault.load();
+  if (f < 0) {
     const char* e = getenv("WIPDB_HCRC_FORCE_FAULT");
-    return e && *e == '1';
-  }();
-  return on;
+    int want = e && *e == '1' ? 1 : 0, expect = -1;
+    g_force_fault.compare_exchange_strong(expect, want);
+    f = g_force_fault.load();
+  }
+  return f == 1;
 }
 #endif
 
 // A lane-packed launch is done: with the test build's forced fault, a fault
 // is counted after it, as a faulting launch would count it.
-int LaunchedLp(hipStream_t st) {
+int LaunchedLp(hipStream_t st, unsigned int* fault) {
   int rc = Launched();
 #ifdef WIPDB_HCRC_TEST_HOOKS
   if (rc == HCRC_OK && ForcedFault()) {
-    hipLaunchKernelGGL(crc32c_lds_fault_probe_kernel, dim3(1), dim3(64), 0, st);
+    hipLaunchKernelGGL(crc32c_lds_fault_probe_kernel, dim3(1), dim3(64), 0, st, fault);
     rc = Launched();
   }
 #else
   (void)st;
+  (void)fault;
 #endif
   return rc;
+}
+
+// The fault word of async launches on `st` (assigned on first use; word 0,
+// shared, once kStreamFaultWords streams have one).  Device view.
+unsigned int* StreamFaultWord(hcrc_ctx* ctx, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(ctx->faults_mu);
+  auto it = ctx->stream_words.find(st);
+  if (it != ctx->stream_words.end()) return ctx->d_fault_words + it->second;
+  if (ctx->stream_words.size() >= kStreamFaultWords) return ctx->d_fault_words;
+  const uint32_t k = 1u + kMaxLanes + static_cast<uint32_t>(ctx->stream_words.size());
+  ctx->stream_words.emplace(st, k);
+  return ctx->d_fault_words + k;
 }
 
 // Descriptor batch on device memory, enqueued on st.  auto_long: kDevice for
@@ -533,7 +570,7 @@ int LaunchedLp(hipStream_t st) {
 // spans by itself); host pieces decide on the host (AutoLongHost).
 int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
                 const uint32_t* init, uint32_t* out, size_t count, int flags, hipStream_t st,
-                AutoLong auto_long) {
+                AutoLong auto_long, unsigned int* fault) {
   const bool mask = (flags & HCRC_MASK_OUTPUT) != 0;
   const bool split_long = (flags & HCRC_SPLIT_LONG) != 0 ||
                           (auto_long == AutoLong::kDevice && (flags & HCRC_SPLIT_SMALL) == 0 &&
@@ -553,6 +590,33 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                          init ? init + pos : nullptr, out + pos, n, 0, mask, st);
     } else {
       const int grid = LdsGrid(ctx, n);
+      if (flags & HCRC_PACKED) {
+        // HCRC_PACKED: the pre-pass checks the batch and cuts its covering
+        // range into C equal byte chunks (first[c]); the packed kernel then
+        // streams it (crc32c_ps.h), or runs the default pipeline when the
+        // pre-pass found the batch not packed
+        const uint32_t C = static_cast<uint32_t>(32 * grid);
+        const size_t bytes = (size_t(C) + 1 + lk::kPsMetaWords) * 4;
+        uint8_t* scratch = nullptr;
+        HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), bytes,
+                                          ctx->scratch_pool, st));
+        uint32_t* meta = reinterpret_cast<uint32_t*>(scratch);
+        uint32_t* first = meta + lk::kPsMetaWords;
+        HCRC_CHECK(hipMemsetAsync(meta, 0, lk::kPsMetaWords * 4, st));
+        const int pgrid = static_cast<int>(
+            std::max<size_t>(1, std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8)));
+        hipLaunchKernelGGL(lk::crc32c_ps_index_kernel, dim3(pgrid), dim3(256), 0, st, off + pos,
+                           len + pos, static_cast<uint64_t>(n), C, first, meta);
+        hipLaunchKernelGGL(init ? lk::crc32c_lds_packed_kernel<1> : lk::crc32c_lds_packed_kernel<0>,
+                           dim3(grid), dim3(lk::kThreads), lk::kLdsBytes, st,
+                           static_cast<const uint8_t*>(base), off + pos, len + pos,
+                           init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n),
+                           mask ? lk::kFlagMask : 0u, ctx->d_image, first, meta, C, fault);
+        rc = LaunchedLp(st, fault);
+        if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
+        if (rc) return rc;
+        continue;
+      }
       // HCRC_BALANCE: byte-balanced contiguous workgroup ranges, two small
       // passes over the length column first (only worth it where the spans'
       // sizes vary: the static deal is exact for equal spans)
@@ -579,8 +643,8 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                          lk::kLdsBytes, st, static_cast<const uint8_t*>(base), off + pos,
                          len + pos, init ? init + pos : nullptr, out + pos,
                          static_cast<uint64_t>(n), mask ? lk::kFlagMask : 0u, ctx->d_image,
-                         bounds);
-      rc = LaunchedLp(st);
+                         bounds, fault);
+      rc = LaunchedLp(st, fault);
       if (scratch && hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
     }
     if (rc) return rc;
@@ -763,7 +827,7 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
                      flags | AutoSplit(host_base, offsets + i, lengths + i, n) |
                          AutoLongHost(lengths + i, n),
-                     st, AutoLong::kNo);
+                     st, AutoLong::kNo, lane.FaultWord());
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
@@ -815,7 +879,7 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
                      flags | AutoSplit(base, offsets + i, lengths + i, n) |
                          AutoLongHost(lengths + i, n),
-                     st, AutoLong::kNo);
+                     st, AutoLong::kNo, lane.FaultWord());
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
@@ -936,6 +1000,14 @@ extern "C" {
 
 int hcrc_abi_version(void) { return HCRC_ABI_VERSION; }
 
+#ifdef WIPDB_HCRC_TEST_HOOKS
+// Test build only (not in the header): the forced fault on (1) or off (0)
+// for the launches that follow, whatever WIPDB_HCRC_FORCE_FAULT says.
+__attribute__((visibility("default"))) void hcrc_test_force_fault(int on) {
+  g_force_fault.store(on ? 1 : 0);
+}
+#endif
+
 int hcrc_device_count(int* count) {
   if (!count) return HCRC_ERR_INVALID;
   int n = 0;
@@ -995,6 +1067,8 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
       reinterpret_cast<const void*>(lk::crc32c_lds_spans_kernel<1>),
       reinterpret_cast<const void*>(lk::crc32c_lds_strided_kernel),
       reinterpret_cast<const void*>(lk::crc32c_lds_verify_kernel),
+      reinterpret_cast<const void*>(lk::crc32c_lds_packed_kernel<0>),
+      reinterpret_cast<const void*>(lk::crc32c_lds_packed_kernel<1>),
       reinterpret_cast<const void*>(lk::crc32c_lds_list_kernel<1, 0>),
       reinterpret_cast<const void*>(lk::crc32c_lds_list_kernel<2, 0>),
       reinterpret_cast<const void*>(lk::crc32c_lds_list_kernel<4, 0>),
@@ -1004,11 +1078,11 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
   };
   for (const void* k : kernels)
     HCRC_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lk::kLdsBytes));
-  ctx->d_faults = lk::LpFaultCounter();
-  if (!ctx->d_faults) return HCRC_ERR_HIP;
-  HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_faults), 8 * (kMaxLanes + 1)));
-  HCRC_CHECK(hipMemcpy(ctx->h_faults, ctx->d_faults, 4, hipMemcpyDeviceToHost));
-  ctx->faults_seen = ctx->h_faults[0];
+  HCRC_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx->fault_words), 4 * kFaultWords,
+                           hipHostMallocCoherent | hipHostMallocMapped));
+  memset(ctx->fault_words, 0, 4 * kFaultWords);
+  HCRC_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_fault_words),
+                                     ctx->fault_words, 0));
   {
     std::vector<uint32_t> img(lk::kImageBytes / 4);
     lk::BuildLdsImage(img.data());
@@ -1028,22 +1102,26 @@ int hcrc_ctx_destroy(hcrc_ctx* ctx) {
     for (const auto& kv : SharedCtxs())
       if (kv.second == ctx) return HCRC_ERR_INVALID;
   }
-  DeviceGuard dg(ctx->device);
-  for (auto& lane : ctx->lanes) {
+  delete ctx;
+  return HCRC_OK;
+}
+
+hcrc_ctx::~hcrc_ctx() {
+  if (device < 0) return;
+  DeviceGuard dg(device);
+  for (auto& lane : lanes) {
     if (lane->stream) (void)hipStreamSynchronize(lane->stream);
     for (Slot& s : lane->slots) s.Free();
     if (lane->stream) (void)hipStreamDestroy(lane->stream);
   }
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->d_image) (void)hipFree(ctx->d_image);
-  if (ctx->h_faults) (void)hipHostFree(ctx->h_faults);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  if (ctx->scratch_pool) {
+  if (stream) (void)hipStreamSynchronize(stream);
+  if (d_image) (void)hipFree(d_image);
+  if (stream) (void)hipStreamDestroy(stream);
+  if (scratch_pool) {
     (void)hipDeviceSynchronize();
-    (void)hipMemPoolDestroy(ctx->scratch_pool);
+    (void)hipMemPoolDestroy(scratch_pool);
   }
-  delete ctx;
-  return HCRC_OK;
+  if (fault_words) (void)hipHostFree(fault_words);
 }
 
 void* hcrc_ctx_stream(hcrc_ctx* ctx) { return ctx ? ctx->stream : nullptr; }
@@ -1053,7 +1131,7 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const u
                const uint32_t* init_crcs, uint32_t* out_crcs, size_t count, int flags) {
   if (!ctx || (count && (!base || !offsets || !lengths || !out_crcs))) return HCRC_ERR_INVALID;
   if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG |
-                HCRC_BALANCE))
+                HCRC_BALANCE | HCRC_PACKED))
     return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
   HCRC_DEVICE(ctx);
@@ -1063,7 +1141,7 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const u
     if (rc == HCRC_OK) rc = lane.FaultsBefore();
     if (rc == HCRC_OK)
       rc = LaunchSpans(ctx, base, offsets, lengths, init_crcs, out_crcs, count, flags,
-                       lane->stream, AutoLong::kDevice);
+                       lane->stream, AutoLong::kDevice, lane.FaultWord());
     if (rc) return rc;
     return lane.CheckFaults();
   }
@@ -1076,13 +1154,14 @@ int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offset
                      size_t count, int flags, void* stream) {
   if (!ctx || !(flags & HCRC_DEVICE_PTRS)) return HCRC_ERR_INVALID;
   if (flags & ~(HCRC_DEVICE_PTRS | HCRC_MASK_OUTPUT | HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG |
-                HCRC_BALANCE))
+                HCRC_BALANCE | HCRC_PACKED))
     return HCRC_ERR_INVALID;
   if (count && (!d_base || !d_offsets || !d_lengths || !d_out_crcs)) return HCRC_ERR_INVALID;
   if (count == 0) return HCRC_OK;
   HCRC_DEVICE(ctx);
-  return LaunchSpans(ctx, d_base, d_offsets, d_lengths, d_init_crcs, d_out_crcs, count, flags,
-                     static_cast<hipStream_t>(stream), AutoLong::kDevice);
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  return LaunchSpans(ctx, d_base, d_offsets, d_lengths, d_init_crcs, d_out_crcs, count, flags, st,
+                     AutoLong::kDevice, StreamFaultWord(ctx, st));
 }
 
 int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride, uint32_t length,
@@ -1094,13 +1173,14 @@ int hcrc_batch_strided_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
   if (count == 0) return HCRC_OK;
   HCRC_DEVICE(ctx);
   const hipStream_t st = static_cast<hipStream_t>(stream);
+  unsigned int* const fault = StreamFaultWord(ctx, st);
   for (size_t pos = 0; pos < count; pos += kMaxLaunchSpans) {
     const size_t n = std::min(count - pos, kMaxLaunchSpans);
     hipLaunchKernelGGL(lk::crc32c_lds_strided_kernel, dim3(LdsGrid(ctx, n)), dim3(lk::kThreads),
                        lk::kLdsBytes, st, static_cast<const uint8_t*>(d_base) + pos * stride,
                        stride, length, init_crc, d_out_crcs + pos, static_cast<uint64_t>(n),
-                       static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_image);
-    const int rc = LaunchedLp(st);
+                       static_cast<uint32_t>(flags & HCRC_MASK_OUTPUT), ctx->d_image, fault);
+    const int rc = LaunchedLp(st, fault);
     if (rc) return rc;
   }
   return HCRC_OK;
@@ -1117,6 +1197,7 @@ int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_of
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const bool split = (flags & HCRC_SPLIT_SMALL) != 0;
   const size_t piece_max = split ? size_t(lk::kMaxListSpans) : kMaxLaunchSpans;
+  unsigned int* const fault = split ? nullptr : StreamFaultWord(ctx, st);
   for (size_t pos = 0; pos < count; pos += piece_max) {
     const size_t n = std::min(count - pos, piece_max);
     int rc;
@@ -1126,8 +1207,9 @@ int hcrc_verify_async_ex(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_of
     } else {
       hipLaunchKernelGGL(lk::crc32c_lds_verify_kernel, dim3(LdsGrid(ctx, n)), dim3(lk::kThreads),
                          lk::kLdsBytes, st, static_cast<const uint8_t*>(d_base), d_offsets + pos,
-                         d_lengths + pos, d_status + pos, static_cast<uint64_t>(n), ctx->d_image);
-      rc = LaunchedLp(st);
+                         d_lengths + pos, d_status + pos, static_cast<uint64_t>(n), ctx->d_image,
+                         fault);
+      rc = LaunchedLp(st, fault);
     }
     if (rc) return rc;
   }
@@ -1205,24 +1287,33 @@ int hcrc_fill_splitmix64_async(hcrc_ctx* ctx, void* d_dst, uint64_t nbytes, uint
 
 int hcrc_ctx_check(hcrc_ctx* ctx) {
   if (!ctx) return HCRC_ERR_INVALID;
-  HCRC_DEVICE(ctx);
-  // the device's count, read after the launches already complete (the caller
-  // synchronised the streams it launched on); slot 0 of the snapshots is the
-  // context's own (lanes use 2 .. 2 kMaxLanes + 1)
-  std::lock_guard<std::mutex> lk(ctx->lanes_mu);
-  HCRC_CHECK(hipMemcpyAsync(ctx->h_faults, ctx->d_faults, 4, hipMemcpyDeviceToHost, ctx->stream));
-  HCRC_CHECK(hipStreamSynchronize(ctx->stream));
-  const unsigned int now = ctx->h_faults[0];
-  return ctx->faults_seen.exchange(now) != now ? HCRC_ERR_KERNEL : HCRC_OK;
+  // every caller stream's word (and the shared word 0), read and cleared:
+  // the caller synchronised the streams it launched on, so their launches
+  // are complete and their stores visible (coherent host memory)
+  std::lock_guard<std::mutex> lk(ctx->faults_mu);
+  unsigned int any = __atomic_exchange_n(ctx->fault_words, 0u, __ATOMIC_SEQ_CST);
+  for (const auto& kv : ctx->stream_words)
+    any |= __atomic_exchange_n(ctx->fault_words + kv.second, 0u, __ATOMIC_SEQ_CST);
+  return any ? HCRC_ERR_KERNEL : HCRC_OK;
 }
 
 int hcrc_sync(hcrc_ctx* ctx, void* stream) {
   if (!ctx) return HCRC_ERR_INVALID;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
   {
     HCRC_DEVICE(ctx);
-    HCRC_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    HCRC_CHECK(hipStreamSynchronize(st));
   }
-  return hcrc_ctx_check(ctx);
+  // this stream's word only (plus the shared word 0 of streams past the
+  // table), read and cleared: another caller's fault stays with its stream
+  std::lock_guard<std::mutex> lk(ctx->faults_mu);
+  unsigned int any = 0;
+  const auto it = ctx->stream_words.find(st);
+  if (it != ctx->stream_words.end())
+    any = __atomic_exchange_n(ctx->fault_words + it->second, 0u, __ATOMIC_SEQ_CST);
+  else if (ctx->stream_words.size() >= kStreamFaultWords)
+    any = __atomic_exchange_n(ctx->fault_words, 0u, __ATOMIC_SEQ_CST);
+  return any ? HCRC_ERR_KERNEL : HCRC_OK;
 }
 
 int hcrc_batch_multi_ex(const int* devices, int ndev, const void* base, const uint64_t* offsets,
