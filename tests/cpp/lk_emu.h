@@ -36,21 +36,27 @@ typedef uint8_t g_u8;
 
 namespace emu {
 
+// A reusable barrier of n threads: an arrival count and a generation the
+// waiters sleep on (futex-backed std::atomic wait: no mutex convoy when the
+// last arrival wakes the other 63 lanes of a wave -- the emulation spends
+// most of its time here)
 struct Barrier {
-  std::mutex m;
-  std::condition_variable cv;
-  int n, count = 0;
-  uint64_t gen = 0;
+  std::atomic<int> count{0};
+  std::atomic<uint32_t> gen{0};
+  int n;
   explicit Barrier(int n_) : n(n_) {}
   void wait() {
-    std::unique_lock<std::mutex> lk(m);
-    const uint64_t g = gen;
-    if (++count == n) {
-      count = 0;
-      ++gen;
-      cv.notify_all();
+    const uint32_t g = gen.load(std::memory_order_acquire);
+    if (count.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {
+      count.store(0, std::memory_order_relaxed);
+      gen.fetch_add(1, std::memory_order_release);
+      gen.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g; });
+      for (int i = 0; i < 128; ++i) {
+        if (gen.load(std::memory_order_acquire) != g) return;
+        std::this_thread::yield();
+      }
+      while (gen.load(std::memory_order_acquire) == g) gen.wait(g, std::memory_order_acquire);
     }
   }
 };
@@ -60,8 +66,8 @@ struct Wave {
 };
 struct Group {
   std::vector<uint8_t> lds;
-  Barrier bar{1024};
-  Wave waves[16];
+  Barrier bar{kThreads};
+  Wave waves[kWaves];
   Group() : lds(163840, 0xCD) {}
 };
 // the DMA source range the test allows, and the first violation
@@ -93,15 +99,15 @@ inline void copy16(uint32_t dst, uint64_t src) {
   memcpy(t_group->lds.data() + dst, reinterpret_cast<const void*>(src), 16);
 }
 
-// Runs kernel() on `grid` workgroups of 1024 lane threads (one workgroup at
+// Runs kernel() on `grid` workgroups of kThreads lane threads (one workgroup at
 // a time, as many as the device has CUs would run at once).
 template <class F>
 inline void launch_blocks(uint32_t grid, const std::vector<uint32_t>& blocks, F kernel) {
   for (uint32_t b : blocks) {
     Group g;
     std::vector<std::thread> th;
-    th.reserve(1024);
-    for (uint32_t t = 0; t < 1024; ++t)
+    th.reserve(kThreads);
+    for (uint32_t t = 0; t < static_cast<uint32_t>(kThreads); ++t)
       th.emplace_back([&, t] {
         t_tid = t;
         t_bid = b;
@@ -117,8 +123,8 @@ inline void launch(uint32_t grid, F kernel) {
   for (uint32_t b = 0; b < grid; ++b) {
     Group g;
     std::vector<std::thread> th;
-    th.reserve(1024);
-    for (uint32_t t = 0; t < 1024; ++t)
+    th.reserve(kThreads);
+    for (uint32_t t = 0; t < static_cast<uint32_t>(kThreads); ++t)
       th.emplace_back([&, t] {
         t_tid = t;
         t_bid = b;

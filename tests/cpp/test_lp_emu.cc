@@ -9,7 +9,7 @@
 // desk, the ring, the queue, the batch packing) before a GPU run.
 // The queue's timeout path is forced once (a hidden record marker and a small
 // spin bound): the launch must report the fault.
-// Build: clang++ -std=c++17 -O1 -pthread -I wipdb_amd/csrc -I tests/cpp.
+// Build: clang++ -std=c++20 -O1 -pthread -I wipdb_amd/csrc -I tests/cpp.
 // Usage: test_lp_emu [--pipe=ea|lp] [case ...]; exit 0 = pass.
 #define WIPDB_LK_EMU 1
 // the queue's spin bound, set per case (run-time in the emulation)
@@ -628,11 +628,11 @@ int main(int argc, char** argv) {
       }
     };
     if (Want(argc, argv, "exact fit packed")) {
-      packed_exact("exact fit packed table blocks", 4097, 4225, 4, 1500, false);
-      packed_exact("exact fit packed verify table blocks", 4096, 4224, 0, 1500, true);
-      packed_exact("exact fit packed 512 B..2 KiB", 512, 2200, 5, 3000, false);
-      packed_exact("exact fit packed verify 300..5000", 300, 5000, 0, 1500, true);
-      packed_exact("exact fit packed 16..64 KiB", 16384, 65536, 5, 300, false);
+      packed_exact("exact fit packed table blocks", 4097, 4225, 4, 600, false);
+      packed_exact("exact fit packed verify table blocks", 4096, 4224, 0, 600, true);
+      packed_exact("exact fit packed 512 B..2 KiB", 512, 2200, 5, 1200, false);
+      packed_exact("exact fit packed verify 300..5000", 300, 5000, 0, 600, true);
+      packed_exact("exact fit packed 16..64 KiB", 16384, 65536, 5, 120, false);
     }
   }
   if (Want(argc, argv, "packed tiny")) {  // single spans and pairs, one window or two
@@ -657,7 +657,7 @@ int main(int argc, char** argv) {
       return o;
     };
     {
-      auto l = lens_of(3000, 512, 2200);
+      auto l = lens_of(1000, 512, 2200);
       RunPacked("packed 512 B..2 KiB", buf.data(), buf.size(), Packed(l, 3, 5), l, nullptr, false, 3, 0,
                 true);
       auto in = inits_of(l.size());
@@ -665,21 +665,21 @@ int main(int argc, char** argv) {
                 true, 2, 0, true);
     }
     {
-      auto l = lens_of(1500, 4097, 4225);
+      auto l = lens_of(500, 4097, 4225);
       RunPacked("packed table blocks", buf.data(), buf.size(), Packed(l, 0, 4), l, nullptr, true, 3, 0,
                 true);
     }
     {
       std::vector<uint64_t> o;
-      for (int i = 0; i < 2000; ++i) o.push_back(4096u * i);
-      RunPacked("packed aligned 4 KiB", buf.data(), buf.size(), o, std::vector<uint32_t>(2000, 4096),
+      for (int i = 0; i < 600; ++i) o.push_back(4096u * i);
+      RunPacked("packed aligned 4 KiB", buf.data(), buf.size(), o, std::vector<uint32_t>(600, 4096),
                 nullptr, false, 3, 0, true);
     }
     {
       const uint32_t B[] = {512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
       std::vector<uint32_t> l;
       uint64_t tot = 0;
-      while (tot < (18u << 20)) {
+      while (tot < (6u << 20)) {
         const uint32_t b = B[rng() % 8 < 5 ? rng() % 4 : 4 + rng() % 4];
         l.push_back(b + static_cast<uint32_t>(rng() % (b / 8 + 1)));
         tot += l.back() + 5;
@@ -688,13 +688,13 @@ int main(int argc, char** argv) {
       RunPacked("packed mix 512 B..72 KiB (inits)", buf.data(), buf.size(), Packed(l, 1, 5), l, &in,
                 false, 4, 0, true);
       RunPacked("packed mix, 4 KiB chunks", buf.data(), buf.size(), Packed(l, 7, 5), l, nullptr, true,
-                3, 4000, true);
+                3, 1500, true);
     }
     {
       // short and empty spans among the stream ones, ragged gaps 0..300,
       // spans of exactly 64 / 65 bytes, words shared across a 0..3-byte gap
       std::vector<uint32_t> l;
-      for (int i = 0; i < 2500; ++i) {
+      for (int i = 0; i < 1000; ++i) {
         const uint32_t r = static_cast<uint32_t>(rng() % 20);
         l.push_back(r == 0 ? 0u : r == 1 ? 1u + static_cast<uint32_t>(rng() % 63)
                    : r == 2 ? 64u : r == 3 ? 65u : 64u + static_cast<uint32_t>(rng() % 3000));
@@ -705,11 +705,11 @@ int main(int argc, char** argv) {
       RunPacked("packed tight gaps 0..3", buf.data(), buf.size(), gaps(l, 2, 0, 3), l, nullptr, false, 3,
                 0, true);
       RunPacked("packed gaps up to 4095, small chunks", buf.data(), buf.size(), gaps(l, 9, 0, 4095),
-                  l, &in, false, 2, 700, true);
+                  l, &in, false, 2, 300, true);
     }
     {
       // exact fit: the last span's last byte is the buffer's last byte
-      auto l = lens_of(2000, 700, 5000);
+      auto l = lens_of(600, 700, 5000);
       const auto o = Packed(l, 0, 4);
       Guarded<uint8_t> d(o.back() + l.back());
       for (size_t i = 0; i < d.n; ++i) d[i] = static_cast<uint8_t>(rng());
@@ -717,7 +717,7 @@ int main(int argc, char** argv) {
     }
     {
       // not packed: the fallback computes them all the same
-      auto l = lens_of(2000, 300, 3000);
+      auto l = lens_of(800, 300, 3000);
       auto o = Packed(l, 3, 5);
       std::swap(o[100], o[101]);
       std::swap(l[100], l[101]);
@@ -726,9 +726,9 @@ int main(int argc, char** argv) {
       o2[500] -= 10;  // overlaps the span before
       RunPacked("not packed: overlap", buf.data(), buf.size(), o2, l, nullptr, false, 3, 0, false);
       auto o3 = Packed(l, 3, 5);
-      for (size_t i = 700; i < o3.size(); ++i) o3[i] += 5000;  // a gap of 5 KiB
+      for (size_t i = 400; i < o3.size(); ++i) o3[i] += 5000;  // a gap of 5 KiB
       RunPacked("not packed: a 5 KiB gap", buf.data(), buf.size(), o3, l, nullptr, false, 3, 0, false);
-      auto l4 = lens_of(3000, 5, 60);
+      auto l4 = lens_of(1200, 5, 60);
       RunPacked("not packed: dense short spans", buf.data(), buf.size(), Packed(l4, 1, 7), l4, nullptr,
                 false, 3, 0, false);
     }

@@ -150,7 +150,7 @@ def test_lane_packed_kernels_emulated(tmp_path):
     if not os.path.exists(clang):
         pytest.skip("ROCm clang++ not present")
     exe = str(tmp_path / "test_lp_emu")
-    subprocess.run([clang, "-std=c++17", "-O1", "-pthread", "-Wno-unused-function",
+    subprocess.run([clang, "-std=c++20", "-O1", "-pthread", "-Wno-unused-function",
                     "-I", os.path.join(REPO, "wipdb_amd", "csrc"), "-I", os.path.join(REPO, "tests", "cpp"),
                     os.path.join(REPO, "tests", "cpp", "test_lp_emu.cc"), "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
