@@ -186,7 +186,8 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
   // ---- desk state (lane j: span d0 + j) ----
   // relative addresses: byte offsets from the chunk's first window W0
   uint32_t a32 = 0, b32 = 0;   // span [a32, b32)
-  uint32_t inj = 0;            // head register
+  uint32_t hw = 0;             // the head word as the stream needs it: bytes before A zeroed,
+                               // the head register ~init * x^(-8 h) XORed in
   uint32_t pe = 0;             // E4 of the previous stream span (start of this one's pre-gap)
   uint32_t tw = 0;             // tail word (bytes [E4, E4 + 4) of memory)
   uint32_t in_r = 0, f_r = 0;  // IN and F at the span's cut
@@ -242,7 +243,7 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       const uint32_t before = l == 0u ? 0u : pb;
       pe = umax(before, pe_carry);
       if (last_desk) pe_end = umax(pe_carry, rdlane(incl, 63));
-      inj = head_register_lane(l, stream ? iv : 0u, a32 - hd);
+      const uint32_t inj = head_register_lane(l, stream ? iv : 0u, a32 - hd);
       tk = (stream ? 1u << 12 : 0u) | ((b32 & 3u) << 8);
       in_r = f_r = 0;
       // tail word: the aligned word holding bytes [E4, B) (in the span's page)
@@ -250,6 +251,10 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       if (stream && (b32 & 3u) != 0u) {
         tw = *reinterpret_cast<const uint32_t*>(W0 + e4);
       }
+      // the head word from memory too (so the page's fix-up is one write)
+      hw = 0;
+      if (stream) hw = *reinterpret_cast<const uint32_t*>(W0 + hd);
+      hw = (hw & ~low_bytes(a32 - hd)) ^ inj;
       // spans off the stream: empty ones (crc = init) and short ones,
       // byte by byte from aligned memory words
       const bool small = v && !stream;
@@ -307,6 +312,10 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       }
       wait_vm<0>();
       loads_landed(tw);
+      loads_landed(hw);
+      // the window has landed: this wave issues ahead of the others' compute
+      // until its next DMA is out (as run_lp / run_ea do)
+      if constexpr (kPrio != 0) lk_prio<kPrio>();
       const uint32_t wrel_end = wr + 4096u;
       // ---- the window's fix-ups by the desk lanes, in its LDS slot ----
       const bool stream = l < dn && ((tk >> 12) & 1u) != 0u;
@@ -326,11 +335,7 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           for (uint32_t p = p0 + 4u * l; p < wrel_end; p += 256u) lds_st_sync(ps_lds_addr(pp.slot, p - wr), 0u);
         }
         // head word: bytes before A masked, the head register injected
-        if (stream && hd >= wr && hd < wrel_end) {
-          const uint32_t ha = ps_lds_addr(pp.slot, hd - wr);
-          const uint32_t v = lds_ld_sync(ha);
-          lds_st_sync(ha, (v & ~low_bytes(a32 - hd)) ^ inj);
-        }
+        if (stream && hd >= wr && hd < wrel_end) lds_st_sync(ps_lds_addr(pp.slot, hd - wr), hw);
         // cut: the stripe of the last stream word
         if (stream && e4 > wr && e4 <= wrel_end) {
           const uint32_t q = (e4 - 4u - wr) >> 2;
@@ -348,9 +353,18 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         const uint32_t o = 16u * pp.cm;
         dma4(W0 + wrel_end, pp.slot, o, o + 1024u, o + 2048u, o + 3072u);
       }
-      // ---- the scan, cut once at te ----
+      if constexpr (kPrio != 0) lk_prio<0>();
+      // ---- the scan ----
       const uint32_t te = ce & 31u;
       W[0] ^= l == 0u ? carry : 0u;
+      const uint64_t cutm = ballot(te != 0u);
+      if (cutm == 0u) {
+        // no span ends in this window (long spans' middles): the plain scan
+        // and the whole-window fold carry the open span on
+        carry = fold<1>(lk, l, scan(lk, W))[0];
+        continue;
+      }
+      // cut once at te
       uint32_t x = W[0], fr = 0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -366,7 +380,6 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       }
       const uint32_t o_r = x;  // the register at the stripe's end (0 after a cut at word 15)
       // ---- the window's segments ----
-      const uint64_t cutm = ballot(te != 0u);
       const uint64_t above = l == 63u ? 0u : (cutm >> (l + 1u)) << (l + 1u);
       const uint32_t nxt = above ? static_cast<uint32_t>(__builtin_ctzll(above)) : 64u;
       const uint32_t v = shift64(lk, k1b, k2b, o_r, nxt - 1u - l);
@@ -378,9 +391,9 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       const uint32_t in_l = (l == 0u ? 0u : q1) ^ (prv == ~0u || prv == 0u ? 0u : q2);
       // carry: the last segment, to the window's end
       {
-        const uint32_t plast = cutm ? 63u - static_cast<uint32_t>(__builtin_clzll(cutm)) : ~0u;
+        const uint32_t plast = 63u - static_cast<uint32_t>(__builtin_clzll(cutm));
         const uint32_t q63 = rdlane(qx, 63);
-        const uint32_t qp = plast == ~0u || plast == 0u ? 0u : rdlane(qx, plast - 1u);
+        const uint32_t qp = plast == 0u ? 0u : rdlane(qx, plast - 1u);
         carry = q63 ^ qp;
       }
       // ---- desk lanes whose span was cut here take IN and F ----
