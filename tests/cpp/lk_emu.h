@@ -157,6 +157,7 @@ inline uint32_t lds_cas(uint32_t a, uint32_t cmp, uint32_t v) {
   __atomic_compare_exchange_n(lds_w(a), &c, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
   return c;
 }
+inline void lds_st(uint32_t a, uint32_t v) { memcpy(lds_base() + a, &v, 4); }
 inline uint32_t lds_ld_sync(uint32_t a) { return __atomic_load_n(lds_w(a), __ATOMIC_SEQ_CST); }
 inline void lds_st_sync(uint32_t a, uint32_t v) { __atomic_store_n(lds_w(a), v, __ATOMIC_SEQ_CST); }
 // the wave's LDS accesses are complete: the lanes meet (a lane thread must

@@ -37,6 +37,8 @@ __device__ __forceinline__ uint32_t lds_cas(uint32_t a, uint32_t cmp, uint32_t v
   __atomic_compare_exchange_n(lds_p(a), &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
   return c;  // the old value
 }
+// a plain LDS store (the wave's own data; ordered by program order)
+__device__ __forceinline__ void lds_st(uint32_t a, uint32_t v) { *lds_p(a) = v; }
 // uncached (another wave may write it)
 __device__ __forceinline__ uint32_t lds_ld_sync(uint32_t a) {
   return __atomic_load_n(lds_p(a), __ATOMIC_RELAXED);

@@ -310,41 +310,43 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         d0 += ngone;
         load_desk();
       }
+      // ---- the window's fix-ups, planned before it lands (the stretch from
+      // its arrival to the next DMA's issue is kept to the LDS work) ----
+      const uint32_t wrel_end = wr + 4096u;
+      const bool stream = l < dn && ((tk >> 12) & 1u) != 0u;
+      const uint32_t e4 = b32 & ~3u, hd = a32 & ~3u;
+      // pre-gap [pe, hd) of the span (trailers, other spans' bytes)
+      uint32_t z0 = umax(pe, wr), z1 = umin(hd, wrel_end);
+      if (!stream) z0 = z1 = 0;
+      const bool gaps = ballot(z0 < z1) != 0u;
+      // after the chunk's last stream span: zeroed by every lane
+      const uint32_t p0 = last_desk ? umax(pe_end, wr) : wrel_end;
+      // head word: bytes before A masked, the head register injected
+      const bool head = stream && hd >= wr && hd < wrel_end;
+      const uint32_t head_a = ps_lds_addr(pp.slot, (hd - wr) & 4095u);
+      // cut: the stripe of the last stream word
+      const bool cut = stream && e4 > wr && e4 <= wrel_end;
+      const uint32_t cq = (e4 - 4u - wr) >> 2;
+      const uint32_t cut_a = PsCutAddr(w, (cq >> 4) & 63u);
       wait_vm<0>();
       loads_landed(tw);
       loads_landed(hw);
       // the window has landed: this wave issues ahead of the others' compute
       // until its next DMA is out (as run_lp / run_ea do)
       if constexpr (kPrio != 0) lk_prio<kPrio>();
-      const uint32_t wrel_end = wr + 4096u;
-      // ---- the window's fix-ups by the desk lanes, in its LDS slot ----
-      const bool stream = l < dn && ((tk >> 12) & 1u) != 0u;
-      const uint32_t e4 = b32 & ~3u, hd = a32 & ~3u;
-      {
-        // pre-gap [pe, hd), and after the chunk's last stream span to the end
-        uint32_t z0 = umax(pe, wr), z1 = umin(hd, wrel_end);
-        if (!stream) z0 = z1 = 0;
+      if (gaps) {
         for (;;) {
           const bool more = z0 < z1;
-          if (ballot(more) == 0u) break;
-          if (more) lds_st_sync(ps_lds_addr(pp.slot, z0 - wr), 0u);
+          if (more) lds_st(ps_lds_addr(pp.slot, z0 - wr), 0u);
           z0 += 4u;
-        }
-        if (last_desk) {
-          const uint32_t p0 = umax(pe_end, wr);
-          for (uint32_t p = p0 + 4u * l; p < wrel_end; p += 256u) lds_st_sync(ps_lds_addr(pp.slot, p - wr), 0u);
-        }
-        // head word: bytes before A masked, the head register injected
-        if (stream && hd >= wr && hd < wrel_end) lds_st_sync(ps_lds_addr(pp.slot, hd - wr), hw);
-        // cut: the stripe of the last stream word
-        if (stream && e4 > wr && e4 <= wrel_end) {
-          const uint32_t q = (e4 - 4u - wr) >> 2;
-          lds_st_sync(PsCutAddr(w, q >> 4), ((q & 15u) + 1u) | (l << 8));
+          if (ballot(z0 < z1) == 0u) break;
         }
       }
+      for (uint32_t p = p0 + 4u * l; p < wrel_end; p += 256u) lds_st(ps_lds_addr(pp.slot, p - wr), 0u);
+      if (head) lds_st(head_a, hw);
+      if (cut) lds_st(cut_a, ((cq & 15u) + 1u) | (l << 8));
       lds_order();  // the fix-ups, then the lanes' reads of the window and the table
-      const uint32_t ce = lds_ld_sync(cut_addr);
-      lds_st_sync(cut_addr, 0u);
+      const uint32_t ce = lds_ld(cut_addr);
       uint32_t W[16];
       pp.read(W);
       pp.release();
@@ -354,6 +356,7 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         dma4(W0 + wrel_end, pp.slot, o, o + 1024u, o + 2048u, o + 3072u);
       }
       if constexpr (kPrio != 0) lk_prio<0>();
+      lds_st(cut_addr, 0u);  // (read above; the next window's marks come after)
       // ---- the scan ----
       const uint32_t te = ce & 31u;
       W[0] ^= l == 0u ? carry : 0u;
@@ -398,8 +401,8 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       }
       // ---- desk lanes whose span was cut here take IN and F ----
       {
-        const bool mine = stream && e4 > wr && e4 <= wrel_end;
-        const uint32_t q = (e4 - 4u - wr) >> 2;
+        const bool mine = cut;
+        const uint32_t q = cq;
         const uint32_t src_l = mine ? q >> 4 : l;
         const uint32_t gi = bperm(in_l, src_l), gf = bperm(fr, src_l);
         if (mine) {
