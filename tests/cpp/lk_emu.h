@@ -266,6 +266,7 @@ inline uint64_t uni_act64(uint64_t v) { return v; }
 inline uint32_t rdlane(uint32_t v, uint32_t k) {
   return static_cast<uint32_t>(emu::xchg(v, [k](const uint64_t* b) { return b[k & 63u]; }));
 }
+inline uint32_t wrlane(uint32_t old, uint32_t v, uint32_t k) { return emu::lane() == (k & 63u) ? v : old; }
 inline uint64_t ballot(bool p) {
   return emu::xchg(p ? 1u : 0u, [](const uint64_t* b) {
     uint64_t m = 0;

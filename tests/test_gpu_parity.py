@@ -830,6 +830,65 @@ def test_packed_promise_broken_falls_back(engine, oracle):
         np.testing.assert_array_equal(got, oracle.batch(host, o, ln))
 
 
+def test_packed_prepass_verdicts():
+    """Which pipeline a HCRC_PACKED batch takes (test build: the pre-pass's
+    words of the last packed launch).  Packed shapes -- 512 B..2 KiB, table
+    blocks, aligned 4 KiB, 64 KiB spans, short / empty spans among them --
+    are streamed (meta[0] == 0); unsorted, overlapping, a 5 KiB gap and
+    dense few-byte spans fall back with the matching kPsBad* bit."""
+    assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
+    code = (
+        "import ctypes, json, numpy as np, torch\n"
+        "from wipdb_amd import Engine, _lib\n"
+        "lib = _lib.load()\n"
+        "rng = np.random.default_rng(8)\n"
+        "def lay(n, lo, hi, g, start=3):\n"
+        "    l = rng.integers(lo, hi + 1, n).astype(np.uint64)\n"
+        "    return start + np.concatenate([[0], np.cumsum(l + g)[:-1]]).astype(np.uint64), l.astype(np.uint32)\n"
+        "cases = {}\n"
+        "cases['512-2k'] = lay(20000, 512, 2200, 5)\n"
+        "cases['tblocks'] = lay(8000, 4097, 4225, 4, 0)\n"
+        "cases['a4k'] = (np.arange(8000, dtype=np.uint64) * 4096, np.full(8000, 4096, np.uint32))\n"
+        "cases['b65536'] = lay(600, 65536, 73728, 5)\n"
+        "o, l = lay(8000, 0, 3000, 7)\n"
+        "cases['shorts'] = (o, l)\n"
+        "o, l = lay(8000, 300, 3000, 5)\n"
+        "o2 = o.copy(); o2[[10, 11]] = o2[[11, 10]]\n"
+        "cases['unsorted'] = (o2, l)\n"
+        "o3 = o.copy(); o3[500] -= 10\n"
+        "cases['overlap'] = (o3, l)\n"
+        "o4 = o.copy(); o4[700:] += 5000\n"
+        "cases['gap5k'] = (o4, l)\n"
+        "cases['dense'] = lay(20000, 5, 60, 7)\n"
+        "res = {}\n"
+        "with Engine(0) as eng:\n"
+        "    size = max(int((o + l).max()) for o, l in cases.values()) + 64\n"
+        "    d = torch.randint(0, 256, (size,), dtype=torch.uint8, device='cuda')\n"
+        "    for k, (o, l) in cases.items():\n"
+        "        do = torch.from_numpy(o.view(np.int64)).cuda()\n"
+        "        dl = torch.from_numpy(l.view(np.int32)).cuda()\n"
+        "        eng.batch_device(d, do, dl, packed=True)\n"
+        "        torch.cuda.synchronize()\n"
+        "        m = (ctypes.c_uint32 * 8)()\n"
+        "        lib.hcrc_test_packed_meta(m, 8)\n"
+        "        res[k] = [int(x) for x in m]\n"
+        "print('META ' + json.dumps(res))\n")
+    env = dict(os.environ, PYTHONPATH=REPO, WIPDB_HCRC_LIB=TEST_LIB)
+    env.pop("WIPDB_HCRC_FORCE_FAULT", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    import json
+    res = json.loads(r.stdout.split("META ", 1)[1].splitlines()[0])
+    print(res)
+    for k in ("512-2k", "tblocks", "a4k", "b65536", "shorts"):
+        assert res[k][0] == 0, (k, res[k])
+        assert res[k][1] % 4096 == 0 and res[k][1] >= 4096, (k, res[k])
+    for k in ("unsorted", "overlap", "gap5k"):
+        assert res[k][0] & 1, (k, res[k])
+    assert res["dense"][0] & 2, res["dense"]
+
+
 def _run_device_packed(engine, buf, offs, lens):
     out = engine.batch_device(_t(buf), _t(np.asarray(offs, np.uint64)),
                               _t(np.asarray(lens, np.uint32)), packed=True)

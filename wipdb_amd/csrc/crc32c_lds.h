@@ -96,6 +96,9 @@ WIPDB_LK_HD constexpr uint32_t SegAuxAddr(uint32_t w) { return kLdsL2 + (128u + 
 
 // Flags of a launch (the HCRC_MASK_OUTPUT value is shared with the C-ABI).
 constexpr uint32_t kFlagMask = 0x2;
+// run_ps: workgroup g takes chunks g, g + G, g + 2G, ... (round robin)
+// instead of the contiguous range [C g / G, C (g + 1) / G)
+constexpr uint32_t kFlagPsRR = 0x100;
 // Fault bits a launch ORs into its error word (a span was left uncomputed;
 // the host returns HCRC_ERR_KERNEL): a queue record whose producer never
 // wrote it, a queue slot never freed for its next record.

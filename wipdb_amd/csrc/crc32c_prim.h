@@ -125,6 +125,13 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t k) {
   return __builtin_amdgcn_readlane(v, k);
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// v_writelane: lane k (uniform) takes the uniform value v, the others keep old
+__device__ __forceinline__ uint32_t wrlane(uint32_t old, uint32_t v, uint32_t k) {
+  uint32_t r = old;
+  // (the lane select through M0: one SGPR operand per VALU on gfx9)
+  asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r) : "s"(v), "{m0}"(k));
+  return r;
+}
 // Per-lane select by a wave mask: m's bit of the lane ? a : b, one
 // v_cndmask_b32 with the mask in an SGPR pair (hipcc lowered some per-lane ?:
 // chains of the batch path into exec-masked branches)

@@ -525,6 +525,9 @@ enum class AutoLong { kNo, kDevice };
 // error word set after it, as the kernel would) -- the HCRC_ERR_KERNEL paths.
 // hcrc_test_force_fault(on) overrides it from then on (per-stream tests).
 std::atomic<int> g_force_fault{-1};
+// the last packed launch's pre-pass words (meta[0]: 0 = streamed, else the
+// kPsBad* bits of the fallback; meta[1..2]: chunk bytes)
+uint32_t g_test_ps_meta[lk::kPsMetaWords];
 bool ForcedFault() {
   int f = g_force_fault.load();
   if (f < 0) {
@@ -595,7 +598,13 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         // range into C equal byte chunks (first[c]); the packed kernel then
         // streams it (crc32c_ps.h), or runs the default pipeline when the
         // pre-pass found the batch not packed
-        const uint32_t C = static_cast<uint32_t>(32 * grid);
+        static const int chunks_per_group = [] {
+          const char* e = getenv("WIPDB_PS_CHUNKS");  // (tuning: chunks per workgroup)
+          const int v = e ? atoi(e) : 0;
+          return v >= 1 && v <= 1024 ? v : 32;
+        }();
+        static const bool ps_rr = getenv("WIPDB_PS_RR") && atoi(getenv("WIPDB_PS_RR")) != 0;
+        const uint32_t C = static_cast<uint32_t>(chunks_per_group * grid);
         const size_t bytes = (size_t(C) + 1 + lk::kPsMetaWords) * 4;
         uint8_t* scratch = nullptr;
         HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), bytes,
@@ -607,11 +616,19 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
             std::max<size_t>(1, std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8)));
         hipLaunchKernelGGL(lk::crc32c_ps_index_kernel, dim3(pgrid), dim3(256), 0, st, off + pos,
                            len + pos, static_cast<uint64_t>(n), C, first, meta);
+#ifdef WIPDB_HCRC_TEST_HOOKS
+        // (test build: the pre-pass's verdict and chunk size, for the tests
+        // that check which pipeline a packed batch took)
+        HCRC_CHECK(hipMemcpyAsync(g_test_ps_meta, meta, sizeof(g_test_ps_meta),
+                                  hipMemcpyDeviceToHost, st));
+        HCRC_CHECK(hipStreamSynchronize(st));
+#endif
         hipLaunchKernelGGL(init ? lk::crc32c_lds_packed_kernel<1> : lk::crc32c_lds_packed_kernel<0>,
                            dim3(grid), dim3(lk::kThreads), lk::kLdsBytes, st,
                            static_cast<const uint8_t*>(base), off + pos, len + pos,
                            init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n),
-                           mask ? lk::kFlagMask : 0u, ctx->d_image, first, meta, C, fault);
+                           (mask ? lk::kFlagMask : 0u) | (ps_rr ? lk::kFlagPsRR : 0u),
+                           ctx->d_image, first, meta, C, fault);
         rc = LaunchedLp(st, fault);
         if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
         if (rc) return rc;
@@ -1005,6 +1022,10 @@ int hcrc_abi_version(void) { return HCRC_ABI_VERSION; }
 // for the launches that follow, whatever WIPDB_HCRC_FORCE_FAULT says.
 __attribute__((visibility("default"))) void hcrc_test_force_fault(int on) {
   g_force_fault.store(on ? 1 : 0);
+}
+// The pre-pass words of the last HCRC_PACKED launch (n <= 8 copied).
+__attribute__((visibility("default"))) void hcrc_test_packed_meta(uint32_t* out, int n) {
+  for (int i = 0; i < n && i < static_cast<int>(lk::kPsMetaWords); ++i) out[i] = g_test_ps_meta[i];
 }
 #endif
 
