@@ -158,6 +158,11 @@ inline uint32_t lds_cas(uint32_t a, uint32_t cmp, uint32_t v) {
   return c;
 }
 inline void lds_st(uint32_t a, uint32_t v) { memcpy(lds_base() + a, &v, 4); }
+inline void lds_st4(uint32_t a, const u32x4& v) {
+  if (a & 15u) abort();  // (ds_write_b128 needs 16-byte alignment here)
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  memcpy(lds_base() + a, w, 16);
+}
 inline uint32_t lds_ld_sync(uint32_t a) { return __atomic_load_n(lds_w(a), __ATOMIC_SEQ_CST); }
 inline void lds_st_sync(uint32_t a, uint32_t v) { __atomic_store_n(lds_w(a), v, __ATOMIC_SEQ_CST); }
 // the wave's LDS accesses are complete: the lanes meet (a lane thread must
@@ -287,6 +292,16 @@ inline uint32_t mbcnt_lo(uint32_t m, uint32_t acc) {
 inline uint32_t mbcnt_hi(uint32_t m, uint32_t acc) {
   const uint32_t l = emu::lane();
   return acc + (l < 32u ? 0u : static_cast<uint32_t>(__builtin_popcount(m & ((1u << (l - 32u)) - 1u))));
+}
+inline uint32_t fperm(uint32_t v, uint32_t dst) {
+  const uint64_t pk = static_cast<uint64_t>(v) | (static_cast<uint64_t>(dst & 63u) << 32);
+  return static_cast<uint32_t>(emu::xchg(pk, [](const uint64_t* b) -> uint64_t {
+    const uint32_t me = emu::lane();
+    uint32_t r = 0;  // (the highest pusher wins; none: 0)
+    for (uint32_t j = 0; j < 64; ++j)
+      if ((b[j] >> 32) == me) r = static_cast<uint32_t>(b[j]);
+    return r;
+  }));
 }
 inline uint32_t bperm_raw(uint32_t v, uint32_t ln) {
   return static_cast<uint32_t>(emu::xchg(v, [ln](const uint64_t* b) { return b[ln & 63u]; }));

@@ -294,6 +294,10 @@ void RunExact(const char* name, Guarded<uint8_t>& data, const std::vector<uint64
 // `data` (any buffer; the DMA range is its pages).  C: chunks of the launch
 // (0: 32 per workgroup, as the host picks).  want_packed: what the pre-pass
 // must decide.
+// the packed launches' flags beyond the mask: kFlagPsOnly keeps them on run_ps
+// where the kernel would hand a batch that suits it to run_ea
+uint32_t g_packed_flags = kFlagPsOnly;
+
 void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std::vector<uint64_t>& offs,
                const std::vector<uint32_t>& lens, const std::vector<uint32_t>* inits, bool mask,
                uint32_t cus, uint32_t C, bool want_packed) {
@@ -332,18 +336,21 @@ void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std:
   emu::g_src_lo = lo & ~uint64_t(4095);
   emu::g_src_hi = (lo + data_n + 4095) & ~uint64_t(4095);
   const uint8_t* img = reinterpret_cast<const uint8_t*>(g_image.data());
+  emu::g_pipes.exchange(0);
   emu::launch(grid, [&] {
     if (inits)
       crc32c_lds_packed_kernel<1>(data, offs.data(), lens.data(), inits->data(), got.data(), n,
-                                  mask ? kFlagMask : 0u, img, first.data(), meta.data(), C,
+                                  (mask ? kFlagMask : 0u) | g_packed_flags, img, first.data(), meta.data(), C,
                                   &g_fault_word);
     else
       crc32c_lds_packed_kernel<0>(data, offs.data(), lens.data(), nullptr, got.data(), n,
-                                  mask ? kFlagMask : 0u, img, first.data(), meta.data(), C,
+                                  (mask ? kFlagMask : 0u) | g_packed_flags, img, first.data(), meta.data(), C,
                                   &g_fault_word);
   });
   char label[96];
-  snprintf(label, sizeof label, "%s [%s]", name, packed ? "ps" : "fallback");
+  const int pipes = emu::g_pipes.load();
+  snprintf(label, sizeof label, "%s [%s]", name,
+           !packed ? "fallback" : ((pipes & 1) != 0 ? "ea" : "ps"));
   if (packed != want_packed) {
     fprintf(stderr, "  %s: the pre-pass says %s (meta %#x)\n", name, packed ? "packed" : "not packed",
             meta[0]);
@@ -668,6 +675,10 @@ int main(int argc, char** argv) {
       auto l = lens_of(500, 4097, 4225);
       RunPacked("packed table blocks", buf.data(), buf.size(), Packed(l, 0, 4), l, nullptr, true, 3, 0,
                 true);
+      g_packed_flags = 0;  // the kernel's own choice: run_ea
+      RunPacked("packed table blocks, dispatched", buf.data(), buf.size(), Packed(l, 0, 4), l, nullptr,
+                true, 3, 0, true);
+      g_packed_flags = kFlagPsOnly;
     }
     {
       std::vector<uint64_t> o;

@@ -830,6 +830,43 @@ def test_packed_promise_broken_falls_back(engine, oracle):
         np.testing.assert_array_equal(got, oracle.batch(host, o, ln))
 
 
+def test_packed_stream_only_matches_default():
+    """The packed kernel hands batches that suit run_ea (aligned 4 KiB blocks,
+    table blocks, spans of >= 16 KiB) to it; with WIPDB_PS_ONLY=1 run_ps takes
+    them too.  Those shapes through run_ps, with inits and the masked output,
+    equal the default pipeline's CRCs (itself checked against the oracle
+    above), over a few hundred MiB each."""
+    code = (
+        "import numpy as np, torch\n"
+        "from wipdb_amd import Engine\n"
+        "rng = np.random.default_rng(12)\n"
+        "def lay(n, lo, hi, g, start=0):\n"
+        "    l = rng.integers(lo, hi + 1, n).astype(np.uint64)\n"
+        "    return start + np.concatenate([[0], np.cumsum(l + g)[:-1]]).astype(np.uint64), l.astype(np.uint32)\n"
+        "cases = {'tblocks': lay(60000, 4097, 4225, 4), 'a4k': (np.arange(60000, dtype=np.uint64) * 4096,\n"
+        "         np.full(60000, 4096, np.uint32)), 'b65536': lay(4000, 65536, 73728, 5, 3),\n"
+        "         'b16k': lay(15000, 16384, 18432, 0, 1)}\n"
+        "bad = []\n"
+        "with Engine(0) as eng:\n"
+        "    size = max(int((o + l).max()) for o, l in cases.values()) + 64\n"
+        "    d = torch.randint(0, 256, (size,), dtype=torch.uint8, device='cuda')\n"
+        "    for k, (o, l) in cases.items():\n"
+        "        do = torch.from_numpy(o.view(np.int64)).cuda()\n"
+        "        dl = torch.from_numpy(l.view(np.int32)).cuda()\n"
+        "        di = torch.from_numpy(rng.integers(0, 2**32, o.size, dtype=np.uint64).astype(np.uint32).view(np.int32)).cuda()\n"
+        "        for inits, m in ((None, False), (di, True)):\n"
+        "            a = eng.batch_device(d, do, dl, inits, mask_output=m, packed=True)\n"
+        "            b = eng.batch_device(d, do, dl, inits, mask_output=m)\n"
+        "            if not bool((a == b).all()):\n"
+        "                bad.append((k, m, int((a != b).sum())))\n"
+        "print('BAD', bad)\n")
+    env = dict(os.environ, PYTHONPATH=REPO, WIPDB_PS_ONLY="1", WIPDB_PS_CHUNKS="16")
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "BAD []" in r.stdout, r.stdout[-2000:]
+
+
 def test_packed_prepass_verdicts():
     """Which pipeline a HCRC_PACKED batch takes (test build: the pre-pass's
     words of the last packed launch).  Packed shapes -- 512 B..2 KiB, table

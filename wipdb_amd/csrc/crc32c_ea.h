@@ -20,6 +20,11 @@
 #include "crc32c_dev.h"
 #include "crc32c_walk.h"
 
+#ifndef LP_T  // (the profiling build's markers, crc32c_lds.hip)
+#define LP_T(x)
+#define LP_ACC(k, v)
+#endif
+
 namespace wipdb {
 namespace lk {
 
@@ -139,14 +144,23 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
     issue(g);
     cur = g.c;
   }
+#ifdef WIPDB_PROF_ON
+  // profiling build: 0 wait, 1 landed -> next DMA out, 2 compute, 4 pages, 7 life
+  uint64_t prof[kProfN] = {};
+  LP_T(t_start);
+#endif
   uint32_t chain = 0;  // register carried between the segments of a span
   bool stored_prev = false;
   g_u32* const out32 = (g_u32*)(reinterpret_cast<uintptr_t>(out));
   g_u8* const out8 = (g_u8*)(reinterpret_cast<uintptr_t>(out));
 
   for (;;) {
+    LP_T(e0);
     if (stored_prev) wait_vm<1>();
     else wait_vm<0>();
+    LP_T(e1);
+    LP_ACC(0, e1 - e0);
+    LP_ACC(4, 1);
     uint32_t W[16];
     pp.read(W);
     u32x4 ax{0, 0, 0, 0};
@@ -187,6 +201,8 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       }
     }
 
+    LP_T(e2);
+    LP_ACC(1, e2 - e1);
     bool did_store = false;
     if (cur.flags() & kEBatch) {
       // ---- a batch of front pieces, one per 4-lane group ----
@@ -299,6 +315,10 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
       }
     }
     stored_prev = did_store;
+#ifdef WIPDB_PROF_ON
+    LP_T(e3);
+    LP_ACC(2, e3 - e2);
+#endif
 
     if (!(nxt.g1 & kEValid)) {
       if (ring.count == 0u) break;
@@ -316,6 +336,15 @@ __device__ __forceinline__ void run_ea(const Src& src, void* out, uint32_t flags
     if (took_pf) prefetch(pf);
     cur = nxt;
   }
+#ifdef WIPDB_PROF_ON
+  LP_T(t_end);
+  prof[7] = t_end - t_start;
+  if (l == 0u) {
+    const uint32_t slot = (group_id() * static_cast<uint32_t>(kWaves) + w) & 4095u;
+    for (int k = 0; k < kProfN; ++k)
+      atomicAdd(&g_lp_prof[slot * kProfN + k], static_cast<unsigned long long>(prof[k]));
+  }
+#endif
 }
 
 }  // namespace lk

@@ -77,6 +77,7 @@ constexpr uint32_t kMiscHeld = 277;    // long spans held by a wave, not taken o
 constexpr uint32_t kMiscQRes = 278;    // queue records pushed and not yet freed (<= kQSlots)
 constexpr uint32_t kMiscFault = 279;   // kFault* bits of the workgroup (run_lp)
 constexpr uint32_t kMiscFaultWord = 280;  // 2 words: the launch's fault word (run_lp)
+constexpr uint32_t kMiscPsProgress = 512;  // 16 words: run_ps, wave w's pages done
 constexpr uint32_t kMiscQInit = 576;   // 256 words: the init_crc of queue record k
 constexpr uint32_t kMiscBytes = 1024 * 4;
 
@@ -87,7 +88,8 @@ constexpr uint32_t kMiscBytes = 1024 * 4;
 //     last word of 0 = a free slot; record k's init_crc in misc word
 //     kMiscQInit + k;
 //   * wave w's aux chunk of a segment tail: the c = 0 column of level-2 row
-//     128 + w (misc words 512.. are unused).
+//     128 + w (misc words 512 .. 575; run_ps, never in the same launch,
+//     keeps its progress words in 512 .. 527).
 constexpr uint32_t kQSlots = 256;
 WIPDB_LK_HD constexpr uint32_t QRecAddr(uint32_t k) {
   return kLdsMain + (k & (kQSlots - 1u)) * 256u + 128u;
@@ -99,6 +101,8 @@ constexpr uint32_t kFlagMask = 0x2;
 // run_ps: workgroup g takes chunks g, g + G, g + 2G, ... (round robin)
 // instead of the contiguous range [C g / G, C (g + 1) / G)
 constexpr uint32_t kFlagPsRR = 0x100;
+// the packed kernel: run_ps even where run_ea suits the batch (tests, A/Bs)
+constexpr uint32_t kFlagPsOnly = 0x200;
 // Fault bits a launch ORs into its error word (a span was left uncomputed;
 // the host returns HCRC_ERR_KERNEL): a queue record whose producer never
 // wrote it, a queue slot never freed for its next record.

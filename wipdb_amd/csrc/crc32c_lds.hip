@@ -37,6 +37,22 @@
 #include <stdint.h>
 
 #include "crc32c_dev.h"
+
+#if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
+// Profiling build only: per wave, the cycles of each part of a pipeline's
+// loop (s_memtime) and its iteration counts, summed over launches
+// (scripts/debug/lp_prof.py, ps_prof.py).
+namespace wipdb {
+namespace lk {
+constexpr int kProfN = 16;  // accumulators per wave
+__device__ unsigned long long g_lp_prof[4096 * kProfN];
+}  // namespace lk
+}  // namespace wipdb
+#define WIPDB_PROF_ON 1
+#define LP_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
+#define LP_ACC(k, v) (prof[k] += (v))
+#endif
+
 #include "crc32c_ea.h"
 
 namespace wipdb {
@@ -226,17 +242,6 @@ __device__ __forceinline__ void report_fault(unsigned int* word, uint32_t) {
 }
 #endif
 
-#if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
-// Profiling build only: per wave, the cycles of each part of run_lp's loop
-// (s_memtime) and its iteration counts, summed over launches.
-constexpr int kProfN = 16;  // accumulators per wave (scripts/debug/lp_prof.py NAMES)
-__device__ unsigned long long g_lp_prof[4096 * kProfN];
-#define LP_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
-#define LP_ACC(k, v) (prof[k] += (v))
-#else
-#define LP_T(x)
-#define LP_ACC(k, v)
-#endif
 
 template <int OUT, typename Src>
 __device__ __forceinline__ void run_lp(const Src& src, void* out, uint32_t flags,
@@ -1060,9 +1065,12 @@ template __global__ void crc32c_lds_spans_kernel<1>(const uint8_t*, const uint64
                                                     uint64_t, uint32_t, const uint8_t*,
                                                     const uint32_t*, unsigned int*);
 
-// Packed batch (HCRC_PACKED, crc32c_ps.h): run_ps when the pre-pass found the
-// batch packed (meta[0] == 0), else the lane-packed pipeline -- a broken
-// promise costs speed, never a CRC.  first / C: the chunk index.
+// Packed batch (HCRC_PACKED, crc32c_ps.h): run_ea when the batch suits it
+// (pick_ea: aligned 4 KiB blocks, table blocks, spans of >= 16 KiB -- where it
+// is 4-7 % faster than run_ps, profiles/r05v_ab.log), else run_ps when the
+// pre-pass found the batch packed (meta[0] == 0), else the lane-packed
+// pipeline -- a broken promise costs speed, never a CRC.  first / C: the
+// chunk index.
 template <int INIT>
 __global__ __launch_bounds__(kThreads) void crc32c_lds_packed_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
@@ -1071,7 +1079,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_packed_kernel(
     const uint32_t* __restrict__ first, const uint32_t* __restrict__ meta, uint32_t C,
     unsigned int* fault) {
   const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u, nullptr};
-  if (meta[0] != 0u) run_lp<0>(src, out, flags, image, fault);
+  if ((flags & kFlagPsOnly) == 0u && pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
+  else if (meta[0] != 0u) run_lp<0>(src, out, flags & kFlagMask, image, fault);
   else run_ps(src, out, flags, image, first, C, fault);
 }
 template __global__ void crc32c_lds_packed_kernel<0>(const uint8_t*, const uint64_t*,
@@ -1102,7 +1111,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_strided_kernel(
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image,
     unsigned int* fault) {
   const StridedSrc src{base, stride, length, init, count};
-  if (pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
+  if ((flags & kFlagPsOnly) == 0u && pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
   else run_lp<0>(src, out, flags & kFlagMask, image, fault);
 }
 

@@ -39,6 +39,10 @@ __device__ __forceinline__ uint32_t lds_cas(uint32_t a, uint32_t cmp, uint32_t v
 }
 // a plain LDS store (the wave's own data; ordered by program order)
 __device__ __forceinline__ void lds_st(uint32_t a, uint32_t v) { *lds_p(a) = v; }
+// a 16-byte store (a 16-byte aligned address: ds_write_b128)
+__device__ __forceinline__ void lds_st4(uint32_t a, const u32x4& v) {
+  *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(static_cast<uintptr_t>(a)) = v;
+}
 // uncached (another wave may write it)
 __device__ __forceinline__ uint32_t lds_ld_sync(uint32_t a) {
   return __atomic_load_n(lds_p(a), __ATOMIC_RELAXED);
@@ -149,6 +153,13 @@ __device__ __forceinline__ uint32_t mbcnt_lo(uint32_t m, uint32_t acc) {
 }
 __device__ __forceinline__ uint32_t mbcnt_hi(uint32_t m, uint32_t acc) {
   return __builtin_amdgcn_mbcnt_hi(m, acc);
+}
+// ds_permute_b32 (a push): lane `dst` receives v.  Every lane active and the
+// dst a permutation of the lanes (gfx950: a lane that two lanes push to keeps
+// the higher one's value; one that none pushes to reads 0)
+__device__ __forceinline__ uint32_t fperm(uint32_t v, uint32_t dst) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_permute(static_cast<int>(dst << 2),
+                                                           static_cast<int>(v)));
 }
 __device__ __forceinline__ uint32_t bperm_raw(uint32_t v, uint32_t lane) {
   return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(lane << 2),

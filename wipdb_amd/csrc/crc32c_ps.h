@@ -61,6 +61,10 @@
 namespace wipdb {
 namespace lk {
 
+#ifndef WIPDB_PS_PRIO
+#define WIPDB_PS_PRIO 3
+#endif
+constexpr int kPsPrio = WIPDB_PS_PRIO;  // wave priority from a page's landing to its next DMA
 constexpr uint32_t kPsDesk = 64;        // spans per desk (one per lane)
 constexpr uint32_t kPsMinStream = 96;   // spans shorter than this are computed off the stream
                                         // (a stream span's stream part is then >= 64 bytes)
@@ -145,6 +149,34 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
   if (bad) global_or(meta, bad);
 }
 
+// A page's events to the lanes of their stripes: the lanes with `ev`
+// (consecutive: the desk's stream spans in rank order, below) each hand
+// `val` (nonzero) to lane `stripe` (distinct, increasing with the lane);
+// the others get 0.  One or two
+// events: readlane / writelane; more: the OR of the stripe bits (DPP), each
+// stripe lane's rank among them (mbcnt) and one ds_bpermute from its desk
+// lane -- a fixed cost, where the per-event chain is a few hundred cycles
+// of dependent scalar / vector hand-offs per event.
+__device__ __forceinline__ uint32_t ps_deliver(uint32_t l, bool ev, uint32_t stripe, uint32_t val) {
+  const uint64_t m = ballot(ev);
+  if (m == 0u) return 0u;
+  if (__builtin_popcountll(m) <= 2) {
+    uint32_t r = 0;
+    for (uint64_t e = m; e != 0u; e &= e - 1u) {
+      const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(e));
+      r = wrlane(r, rdlane(val, j), rdlane(stripe, j));
+    }
+    return r;
+  }
+  const uint32_t lo = scan_or(ev && stripe < 32u ? 1u << stripe : 0u);
+  const uint32_t hi = scan_or(ev && stripe >= 32u ? 1u << (stripe - 32u) : 0u);
+  const uint32_t k = mbcnt_hi(hi, mbcnt_lo(lo, 0u));  // event stripes below the lane
+  const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(m)) + k;
+  const uint32_t v = bperm(val, j & 63u);
+  const bool mine = ((l < 32u ? lo >> l : hi >> (l - 32u)) & 1u) != 0u;
+  return mine ? v : 0u;
+}
+
 // ---------------------------------------------------------------------------
 // run_ps.  Src: DescSrc (offsets, lengths, inits).
 // ---------------------------------------------------------------------------
@@ -160,7 +192,10 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
   const uint32_t c_hi = rr ? (C > g ? (C - g + G - 1u) / G : 0u)
                            : static_cast<uint32_t>(static_cast<uint64_t>(C) * (g + 1u) / G);
   if (c_lo >= c_hi) return;
-  load_image(image, w, l);
+  // the wave's progress word (pages done), read by the others (below)
+  const uint32_t prog_addr = MiscAddr(kMiscPsProgress + w);
+  lds_st_sync(prog_addr, 0u);
+  load_image(image, w, l);  // (its barrier: every progress word is 0 before any is read)
   const Lane lk = make_lane<1>(l);
   Pipe pp;
   pp.init(l, w);
@@ -178,22 +213,33 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
   const uint32_t dma_o = 16u * pp.cm;
 
   // ---- desk state (lane j: span d0 + j), relative to the chunk's W0 ----
-  // A stream span [a, b) is its stream words [a & ~3, E16 = b & ~15) and a
-  // tail of k16 = b - E16 < 16 bytes (loaded from memory with the desk): its
-  // last stream word is the last of a 16-byte chunk, so the scan can only
-  // have to cut after word 3, 7, 11 or 15 of a stripe.
+  // A stream span [a, b) is its stream chunks [H16 = a & ~15, E16 = b & ~15)
+  // and a tail of k16 = b - E16 < 16 bytes (loaded from memory with the
+  // desk).  Its head chunk is rewritten in the page (bytes before a zeroed,
+  // ~init * x^(-8 (a - H16)) XORed in) and the scan of the stripe holding it
+  // starts that chunk from register 0 (a RESET); the stripe holding its last
+  // chunk keeps the register after it (F) and starts again from 0 (a CUT).
+  // Bytes between a cut and the next reset (trailers, short spans, a chunk's
+  // front) are never zeroed: what they leave in the registers no segment uses.
   uint32_t a32 = 0, b32 = 0;      // span [a32, b32)
-  uint32_t hw = 0;                // its head word: bytes before A zeroed, ~init * x^(-8 h) XORed in
-  uint32_t pe = 0;                // E16 of the previous stream span: its pre-gap is [pe, hd)
-  u32x4 tt{0, 0, 0, 0};           // the tail chunk [E16, E16 + 16) from memory
+  u32x4 hc{0, 0, 0, 0};           // its head chunk, rewritten
+  u32x4 tt{0, 0, 0, 0};           // its tail chunk [E16, E16 + 16) from memory
   uint32_t in_r = 0, f_r = 0;     // IN and F at its cut
-  uint32_t hwin = 0, cwin = 0;    // the pages (relative indices) of its head word and its cut
-  uint32_t ha = 0, cs = 0, cv = 0;  // LDS address of the head word; cut stripe, tc | lane << 8
-  uint32_t st = 0;                // bit 0: a stream span; bit 1: it has a pre-gap
+  uint32_t hwin = 0, cwin = 0;    // the pages (relative indices) of its head chunk and its cut
+  uint32_t ha = 0;                // the LDS address of its head chunk in the slot
+  uint32_t cs = 0;                // cut stripe
+  uint32_t cv = 0;                // tc: the cut after stripe chunk tc - 1 (1..4)
+  // the page events of the desk's stream spans in rank order (lane r: the
+  // r-th stream span; then the others): page << 12 | stripe << 3 | value,
+  // value = tc for a cut, reset boundary + 1 for a head; ~0 for none
+  uint32_t cev = ~0u, hev = ~0u;
+  bool sstream = false;           // a stream span
   uint32_t id = 0;
+  uint32_t pages = 0;   // pages done (all chunks)
+  uint32_t behind = 0;  // the wave's priority outside a page's landing: waves ahead of it / 4
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
   // profiling build: 0 wait, 1 landed -> next DMA out, 2 compute, 3 desk
-  // loads, 4 pages, 5 pages with a cut, 6 chunk starts, 7 life, 8 finish,
+  // loads, 4 pages, 5 pages with a cut, 6 plan, 7 life, 8 finish,
   // 9 chunks
   uint64_t prof[kProfN] = {};
   LP_T(t_start);
@@ -213,11 +259,10 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
     const uint64_t b_last = sbase + src.off[s_hi - 1u] + src.len[s_hi - 1u];
     const uint64_t W0 = a_first & ~uint64_t(4095);
     const uint32_t wend = static_cast<uint32_t>(((b_last + 4095u) & ~uint64_t(4095)) - W0);
-    // the first window's DMA right away (the desk loads go out behind it)
-    dma4(W0, pp.slot, dma_o, dma_o + 1024u, dma_o + 2048u, dma_o + 3072u);
+    // the first window's DMA right away (the desk loads go out behind it;
+    // none when the chunk is empty spans at a page-aligned end)
+    if (wend != 0u) dma4(W0, pp.slot, dma_o, dma_o + 1024u, dma_o + 2048u, dma_o + 3072u);
     uint32_t d0 = s_lo, dn = 0;
-    uint32_t pe_carry = 0;  // E16 of the last stream span before the desk
-    uint32_t pe_end = 0;    // E16 of the chunk's last stream span (its last desk)
     bool last_desk = false;
     uint32_t carry = 0;
     uint32_t wr = 0;
@@ -227,7 +272,7 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
     // k16 bytes, ~, Mask, store
     auto finish = [&](uint64_t done) {
       const bool me = ((done >> l) & 1u) != 0u;
-      const uint32_t t = 4u * (cv & 7u);
+      const uint32_t t = 4u * cv;
       uint32_t r = in_r;
       for (uint32_t i = 0; i < 16u; ++i) {
         const bool go = me && i < t;
@@ -267,26 +312,28 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         b32 = v ? a32 + n : wend;
         id = d0 + l;
         const bool stream = v && n >= kPsMinStream;
-        const uint32_t e16 = b32 & ~15u, hd = a32 & ~3u;
-        // the previous stream span's E16 (exclusive max over the lanes before)
-        const uint32_t incl = scan_max(stream ? e16 : 0u);
-        const uint32_t pb = bperm(incl, l == 0u ? 0u : l - 1u);  // (every lane: a wave op)
-        pe = umax(l == 0u ? 0u : pb, pe_carry);
-        if (last_desk) pe_end = umax(pe_carry, rdlane(incl, 63));
-        const uint32_t inj = head_register_lane(l, stream ? iv : 0u, a32 - hd);
-        st = (stream ? 1u : 0u) | (stream && pe < hd ? 2u : 0u);
+        sstream = stream;
+        const uint32_t e16 = b32 & ~15u, h16 = a32 & ~15u, hb = a32 - h16;
+        const uint32_t inj = head_register_lane(l, stream ? iv : 0u, hb);
         in_r = f_r = 0;
-        // the page events: head word, cut (the last stream chunk's stripe)
+        // the page events: head chunk (a reset), last chunk (a cut)
         const uint32_t lc = e16 - 16u;
-        hwin = stream ? hd >> 12 : ~0u;
+        hwin = stream ? h16 >> 12 : ~0u;
         cwin = stream ? lc >> 12 : ~0u;
-        ha = ps_lds_addr(pp.slot, hd & 4095u);
+        ha = ps_lds_addr(pp.slot, h16 & 4095u);
         cs = (lc & 4095u) >> 6;
-        cv = (((lc & 63u) >> 4) + 1u) | (l << 8);
-        // head word and tail chunk from memory (each in the span's pages)
-        hw = 0;
-        if (stream) hw = *reinterpret_cast<const uint32_t*>(W0 + hd);
-        hw = (hw & ~low_bytes(a32 - hd)) ^ inj;
+        cv = ((lc & 63u) >> 4) + 1u;
+        {
+          const uint64_t sm = ballot(stream);
+          const uint32_t nst = static_cast<uint32_t>(__builtin_popcountll(sm));
+          const uint32_t rk = stream ? mbcnt_hi(static_cast<uint32_t>(sm >> 32), mbcnt_lo(static_cast<uint32_t>(sm), 0u))
+                                     : nst + mbcnt_hi(static_cast<uint32_t>(~sm >> 32), mbcnt_lo(static_cast<uint32_t>(~sm), 0u));
+          cev = fperm(stream ? (lc >> 12) << 12 | cs << 3 | cv : ~0u, rk);
+          hev = fperm(stream ? (h16 >> 12) << 12 | ((h16 & 4095u) >> 6) << 3 | (((h16 & 63u) >> 4) + 1u) : ~0u, rk);
+        }
+        // head and tail chunks from memory (each in the span's pages)
+        hc = u32x4{0, 0, 0, 0};
+        if (stream) hc = *reinterpret_cast<const u32x4*>(W0 + h16);
         tt = u32x4{0, 0, 0, 0};
         if (stream && (b32 & 15u) != 0u) tt = *reinterpret_cast<const u32x4*>(W0 + e16);
         // spans off the stream: empty ones (crc = init) and short ones,
@@ -304,6 +351,13 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           const uint32_t crc = ~r;
           if (small) out32[id] = msk ? mask_crc(crc) : crc;
         }
+        // the head chunk in its stream form: the bytes before a zeroed, the
+        // head register XORed into its first word
+        loads_landed(hc);
+        hc.x = (hb >= 4u ? 0u : hc.x & ~low_bytes(hb)) ^ inj;
+        hc.y = hb >= 8u ? 0u : (hb <= 4u ? hc.y : hc.y & ~low_bytes(hb - 4u));
+        hc.z = hb >= 12u ? 0u : (hb <= 8u ? hc.z : hc.z & ~low_bytes(hb - 8u));
+        hc.w = hb <= 12u ? hc.w : hc.w & ~low_bytes(hb - 12u);
       }
       // the windows this desk covers: up to the one where its last span
       // starts (the next span may start there)
@@ -311,80 +365,69 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           last_desk ? wend : umin(wend, uni(rdlane(a32, dn - 1u)) & ~4095u);
       LP_T(dk1);
       LP_ACC(3, dk1 - dk0);
-      const bool sstream = (st & 1u) != 0u;
-      for (; wr < wstop; wr += 4096u) {
-        // ---- the page's fix-ups, planned before it lands ----
-        const uint32_t wi = wr >> 12, wrel_end = wr + 4096u;
+      for (; wr < wstop; wr += 4096u, ++pages) {
+        // ---- the page's events, planned before it lands: resets and cuts
+        // to their stripes' lanes (rz: reset before chunk rz - 1, 0 = none;
+        // tc: cut after chunk tc - 1, 0 = none) ----
+        LP_T(p0);
+        const uint32_t wi = wr >> 12;
         const bool head = hwin == wi;
         const bool cut = cwin == wi;
-        const bool gap = (st & 2u) != 0u && pe < wrel_end && (a32 & ~3u) > wr;
-        const bool gaps = ballot(gap) != 0u;
-        const bool post = last_desk && pe_end < wrel_end;
-        // the cuts to their stripes' lanes (tc: after chunk tc, 0 = none)
-        uint32_t tc = 0;
-        for (uint64_t cm = ballot(cut); cm != 0u; cm &= cm - 1u) {
-          const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(cm));
-          tc = wrlane(tc, rdlane(cv, j) & 7u, rdlane(cs, j));
-        }
+        const uint32_t tc = ps_deliver(l, cev != ~0u && (cev >> 12) == wi, (cev >> 3) & 63u, cev & 7u);
+        const uint32_t rz = ps_deliver(l, hev != ~0u && (hev >> 12) == wi, (hev >> 3) & 63u, hev & 7u);
         LP_T(w0);
+        LP_ACC(6, w0 - p0);
         wait_vm<0>();
         LP_T(w1);
         LP_ACC(0, w1 - w0);
         LP_ACC(4, 1);
-        loads_landed(hw);
-        loads_landed(tt);
         // the page has landed: this wave issues ahead of the others' compute
         // until its next DMA is out (as run_lp does)
-        if constexpr (kPrio != 0) lk_prio<kPrio>();
-        if (gaps) {
-          // each lane the first 8 words of its gap (trailers, tails: a few
-          // words), the wave together the rest of longer ones (a chunk's
-          // first page in front of its first span)
-          const uint32_t z0 = umax(pe, wr);
-          const uint32_t z1 = umin(a32 & ~3u, wrel_end);
-          for (uint32_t p = z0;; p += 4u) {
-            const bool go = gap && p < z1;
-            if (ballot(go) == 0u || p >= z0 + 32u) break;
-            if (go) lds_st(ps_lds_addr(pp.slot, p - wr), 0u);
-          }
-          uint64_t big = ballot(gap && z1 > z0 + 32u);
-          while (big != 0u) {
-            const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(big));
-            big &= big - 1u;
-            const uint32_t b = rdlane(z1, j);
-            for (uint32_t p = rdlane(z0, j) + 32u + 4u * l; p < b; p += 256u)
-              lds_st(ps_lds_addr(pp.slot, p - wr), 0u);
-          }
-        }
-        if (post) {
-          for (uint32_t p = umax(pe_end, wr) + 4u * l; p < wrel_end; p += 256u)
-            lds_st(ps_lds_addr(pp.slot, p - wr), 0u);
-        }
-        if (head) lds_st(ha, hw);
-        lds_order();  // the fix-ups, then the lanes' reads of the page
+        if constexpr (kPsPrio != 0) lk_prio<kPsPrio>();
+        if (head) lds_st4(ha, hc);
+        lds_order();  // the head chunks, then the lanes' reads of the page
         uint32_t W[16];
         pp.read(W);
         pp.release();
         // ---- the next page's DMA ----
-        if (wrel_end < wend) dma4(W0 + wrel_end, pp.slot, dma_o, dma_o + 1024u, dma_o + 2048u, dma_o + 3072u);
-        if constexpr (kPrio != 0) lk_prio<0>();
+        if (wr + 4096u < wend) dma4(W0 + wr + 4096u, pp.slot, dma_o, dma_o + 1024u, dma_o + 2048u, dma_o + 3072u);
+        if constexpr (kPsPrio != 0) {
+          if (behind == 0u) lk_prio<0>();
+          else if (behind == 1u) lk_prio<1>();
+          else if (behind == 2u) lk_prio<2>();
+          else lk_prio<3>();
+        }
         LP_T(w2);
         LP_ACC(1, w2 - w1);
+        // ---- progress: every 4 pages the wave compares its pages with its
+        // workgroup's other waves and takes a priority by how many are ahead
+        // (the SIMDs' oldest-first issue otherwise makes a wave's speed its
+        // age: up to 15 % between the first and the last wave of a SIMD on
+        // equal byte shares) ----
+        if ((pages & 3u) == 3u) {
+          if (l == 0u) lds_st_sync(prog_addr, pages);
+          const uint32_t pv = l < static_cast<uint32_t>(kWaves) ? lds_ld_sync(MiscAddr(kMiscPsProgress + l)) : 0u;
+          const uint32_t ahead = static_cast<uint32_t>(
+              __builtin_popcountll(ballot(l < static_cast<uint32_t>(kWaves) && pv > pages)));
+          behind = umin(3u, ahead * 4u / static_cast<uint32_t>(kWaves));
+        }
         // ---- the scan ----
-        W[0] ^= l == 0u ? carry : 0u;
-        const uint64_t cutm = ballot(tc != 0u);
+        const uint64_t cutm = ballot(tc != 0u), resm = ballot(rz != 0u);
+        // lane 0's register enters from the previous page unless a span
+        // starts at the page (a reset before its chunk 0)
+        const bool r0 = (resm & 1u) != 0u && rdlane(rz, 0) == 1u;
+        W[0] ^= l == 0u && !r0 ? carry : 0u;
         const bool at_end = cutm == (uint64_t(1) << 63) && rdlane(tc, 63) == 4u;
-        if (cutm == 0u || at_end) {
-          // no span ends in this page (long spans' middles): the plain scan
-          // and the whole-page fold carry the open span on; or the one that
-          // ends does so at the page's end (aligned blocks): the fold is its
-          // register, and nothing is carried
+        if ((cutm == 0u || at_end) && (resm == 0u || (resm == 1u && r0))) {
+          // no span ends in this page but at its end (aligned blocks) and
+          // none starts but at its start: the plain scan and the whole-page
+          // fold give the open span's register at the page's end
           const uint32_t r = fold<1>(lk, l, scan(lk, W))[0];
           carry = at_end ? 0u : r;
           if (at_end && cut) {
             in_r = r;
             f_r = 0;
-            cv &= ~7u;  // (no words after IN)
+            cv = 0;  // (no words after IN)
           }
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
           LP_T(w3);
@@ -400,26 +443,31 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           const uint32_t a2 = lds_ld(kLdsMain + vperm(lk.km, x, lk.sel[2]));
           const uint32_t a3 = lds_ld(kLdsMain + vperm(lk.km, x, lk.sel[3]));
           uint32_t y = xor3(a0, a1, a2) ^ a3;  // the register after word i
-          if ((i & 3) == 3) {  // a chunk's end: the cut may be here
+          if ((i & 3) == 3) {  // a chunk's end: a cut, a reset may be here
             const bool c = tc == static_cast<uint32_t>((i >> 2) + 1);
             fr = c ? y : fr;
-            y = c ? 0u : y;
+            y = c || rz == static_cast<uint32_t>((i >> 2) + 2) ? 0u : y;
           }
           x = i < 15 ? y ^ W[i + 1 < 16 ? i + 1 : 15] : y;
         }
-        const uint32_t o_r = x;  // the register at the stripe's end (0 after a cut at word 15)
-        // ---- the page's segments ----
+        // (a reset before chunk 0 of lanes > 0: their register from the
+        // previous stripes is left out below, as the segment starts there)
+        const uint32_t o_r = x;  // the register at the stripe's end
+        // ---- the page's segments: a span's register enters its cut stripe
+        // L from the stripes since its reset stripe R (or the page's start):
+        // IN_L = XOR over l in [R, L) of O_l * x^(8 * 64 (L - 1 - l)) ----
         const uint64_t above = l == 63u ? 0u : (cutm >> (l + 1u)) << (l + 1u);
         const uint32_t nxt = above ? static_cast<uint32_t>(__builtin_ctzll(above)) : 64u;
         const uint32_t v = shift64(lk, k1b, k2b, o_r, nxt - 1u - l);
         const uint32_t qx = scan_xor(v);
-        const uint64_t below = cutm & ((uint64_t(1) << l) - 1u);
+        const uint64_t below = resm & ((uint64_t(1) << l) - 1u);
         const uint32_t prv = below ? 63u - static_cast<uint32_t>(__builtin_clzll(below)) : 0u;
         const uint32_t q1 = bperm(qx, l == 0u ? 0u : l - 1u);
         const uint32_t q2 = bperm(qx, prv == 0u ? 0u : prv - 1u);
         const uint32_t in_l = (l == 0u ? 0u : q1) ^ (prv == 0u ? 0u : q2);
-        {  // the carry: the last segment, to the page's end
-          const uint32_t plast = 63u - static_cast<uint32_t>(__builtin_clzll(cutm));
+        {  // the carry: the span open at the page's end, from its reset
+           // stripe (a cut after the last reset: no span is open)
+          const uint32_t plast = resm ? 63u - static_cast<uint32_t>(__builtin_clzll(resm)) : 0u;
           const uint32_t q63 = rdlane(qx, 63);
           const uint32_t qp = plast == 0u ? 0u : rdlane(qx, plast - 1u);
           carry = q63 ^ qp;
@@ -448,7 +496,6 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       finish(ballot(done && sstream));
       LP_T(f1);
       LP_ACC(8, f1 - f0);
-      pe_carry = umax(pe_carry, rdlane(scan_max(done && sstream ? (b32 & ~15u) : 0u), 63));
       if (ngone == 0u) {  // (cannot happen in a checked batch: at most 63 spans meet a page)
         report_fault(fault, kFaultPsDesk);
         return;
@@ -457,7 +504,7 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
     }
     // ---- the chunk's end: every stream span of its last desk ----
     LP_T(f0);
-    finish(ballot(l < dn && (st & 1u) != 0u));
+    finish(ballot(l < dn && sstream));
     LP_T(f1);
     LP_ACC(8, f1 - f0);
   }

@@ -601,9 +601,11 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         static const int chunks_per_group = [] {
           const char* e = getenv("WIPDB_PS_CHUNKS");  // (tuning: chunks per workgroup)
           const int v = e ? atoi(e) : 0;
-          return v >= 1 && v <= 1024 ? v : 32;
+          return v >= 1 && v <= 1024 ? v : 16;  // one chunk per wave (progress-balanced)
         }();
         static const bool ps_rr = getenv("WIPDB_PS_RR") && atoi(getenv("WIPDB_PS_RR")) != 0;
+        // (tests, A/Bs: the stream-tiled pipeline even where run_ea suits the batch)
+        static const bool ps_only = getenv("WIPDB_PS_ONLY") && atoi(getenv("WIPDB_PS_ONLY")) != 0;
         const uint32_t C = static_cast<uint32_t>(chunks_per_group * grid);
         const size_t bytes = (size_t(C) + 1 + lk::kPsMetaWords) * 4;
         uint8_t* scratch = nullptr;
@@ -627,7 +629,8 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                            dim3(grid), dim3(lk::kThreads), lk::kLdsBytes, st,
                            static_cast<const uint8_t*>(base), off + pos, len + pos,
                            init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n),
-                           (mask ? lk::kFlagMask : 0u) | (ps_rr ? lk::kFlagPsRR : 0u),
+                           (mask ? lk::kFlagMask : 0u) | (ps_rr ? lk::kFlagPsRR : 0u) |
+                               (ps_only ? lk::kFlagPsOnly : 0u),
                            ctx->d_image, first, meta, C, fault);
         rc = LaunchedLp(st, fault);
         if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
