@@ -11,44 +11,57 @@
 // 4 KiB block (global_load_lds_dwordx4, fully coalesced, no per-lane source
 // exchange) and lane l checksums stripe [64 l, 64 l + 64) of it.
 //
-// Span boundaries are made harmless in the window itself, before the lanes
-// read it: the lanes of the wave's desk (one span each) zero the gap bytes
-// in front of their span (trailers, other spans' bytes), mask the bytes in
-// front of its first byte and XOR its head register ~init * x^(-8 h) into its
-// first word (ds_* on the slot), and hand the lane of the stripe that holds
-// its last stream word the cut's position (v_writelane, no LDS).  A span of n bytes at A is its STREAM words [A & ~3,
-// E4 = (A + n) & ~3) plus a tail of k = (A + n) & 3 bytes, which the desk lane
-// loads from memory and feeds at the end (one slicing step).  A lane's scan
-// over its 16 words then only has to cut once: at the stripe's span end (at
-// most one -- stream spans are >= 64 bytes), where it keeps the register F
-// and starts again from 0.  Per window:
+// A stream span [a, b) (>= 96 bytes) is its STREAM CHUNKS [H16 = a & ~15,
+// E16 = b & ~15) -- 16-byte chunks of the page -- plus a tail of b - E16 < 16
+// bytes, which the desk lane loads from memory and feeds at the end.  Its
+// boundaries become two events of the scan, both at chunk boundaries:
 //
-//   O_l   the register at the end of stripe l (the span open there, or 0),
+//   RESET  the desk lane rewrites the span's head chunk in the page (bytes
+//          before a zeroed, ~init * x^(-8 (a - H16)) XORed into its first
+//          word: one ds_write_b128), and the lane of the stripe holding it
+//          starts that chunk from register 0;
+//   CUT    the lane of the stripe holding the span's last chunk keeps the
+//          register after it (F) and goes on from 0.
+//
+// Bytes between a cut and the next reset -- trailers, short spans, a chunk's
+// front -- are never zeroed: what they leave in the registers reaches no
+// segment.  The desk hands each page's events to their stripes' lanes before
+// the page lands (v_writelane for one or two; else the OR of the event
+// stripes, each lane's rank among them (mbcnt) and one ds_bpermute from the
+// desk's stream spans in rank order, laid out once per desk by ds_permute).
+// Per page:
+//
+//   O_l   the register at the end of stripe l (from its reset, or from 0
+//         after a cut),
 //   IN_L  for a cut lane L: the register entering stripe L of its span =
-//         XOR over the lanes l of its segment (from the previous cut lane to
-//         L - 1) of O_l * x^(8 * 64 (L - 1 - l)) -- each lane shifts its O
-//         by whole stripes (the two fold-table levels, shift64) and one wave
-//         prefix XOR gives every segment (the reference's CombineCRC identity,
-//         kv/src/util/crc32c.cc:640-657, at stripe granularity),
-//   carry the register of the span still open at the window's end, XORed
-//         into word 0 of the next window by lane 0.
+//         XOR over the lanes l from its reset stripe R (or the page's start)
+//         to L - 1 of O_l * x^(8 * 64 (L - 1 - l)) -- each lane shifts its O
+//         by whole stripes to the next cut (the two fold-table levels,
+//         shift64) and one wave prefix XOR q gives IN_L = q[L-1] ^ q[R-1]
+//         (the reference's CombineCRC identity, kv/src/util/crc32c.cc:640-657,
+//         at stripe granularity),
+//   carry the register of the span open at the page's end (from the last
+//         reset), XORed into word 0 of the next page by lane 0.
 //
-// The register at a span's end is IN * x^(32 t) ^ F (t = its words in the cut
-// stripe) -- a per-span shift of 1 .. 16 words, deferred to the desk's end,
-// when all its lanes run it at once (one 16-step pass per 64 spans), then
-// the tail step, ~, Mask and the store.  Spans of fewer than 64 bytes (and
-// empty ones) are not in the stream: their bytes are zeroed as gap and the
-// desk lane computes them from memory (rare: a table's metaindex block).
+// A page with no event but a reset at its start and a cut at its end (long
+// spans' middles, aligned blocks) takes the plain scan and the whole-page
+// fold.  The register at a span's end is IN * x^(32 t) ^ F (t = its words in
+// the cut stripe) -- a per-span shift of 4 .. 16 words, deferred to the
+// desk's end, when all its lanes run it at once, then the tail, ~, Mask and
+// the store.  Spans of fewer than 96 bytes (and empty ones) are not in the
+// stream: the desk lane computes them from memory (rare: a table's
+// metaindex block).
 //
-// Work: the pre-pass (ps_index_kernel; the host does it for host batches)
-// checks the batch (sorted, no overlap, gaps < 4 KiB, at most 62 spans
-// starting in any 4 KiB) and cuts the covering range into C equal byte
-// chunks, first[c] = the first span starting in chunk c.  Workgroup g takes
-// chunks [g C / G, (g + 1) C / G) -- equal bytes, whatever the sizes -- and
-// its waves take them one at a time; a chunk is its spans, whole (the range
-// a wave reads ends at its last span's end).  A batch that fails the check
-// runs the lane-packed pipeline (run_lp) instead: HCRC_PACKED is a promise the
-// kernel verifies, never a way to a wrong CRC.
+// Work: the pre-pass (ps_index_kernel) checks the batch (sorted, no overlap,
+// gaps < 4 KiB, at most 62 spans starting in any 4 KiB) and cuts the
+// covering range into C equal byte chunks, first[c] = the first span starting
+// in chunk c: one chunk per wave (C = 16 per workgroup); a chunk is its
+// spans, whole.  The SIMDs issue oldest-first, which on equal shares makes a
+// wave's speed its age (the last wave of a SIMD up to 15 % behind the first):
+// every 4 pages a wave compares its pages with its workgroup's and takes a
+// priority by how many are ahead.  A batch that fails the check runs the
+// default pipelines instead: HCRC_PACKED is a promise the kernel verifies,
+// never a way to a wrong CRC.
 //
 // Reference function: kv::crc32c::Extend (kv/src/util/crc32c.h:24,
 // crc32c.cc:1225-1227) per block span, as WriteRawBlock
@@ -460,25 +473,24 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         const uint32_t nxt = above ? static_cast<uint32_t>(__builtin_ctzll(above)) : 64u;
         const uint32_t v = shift64(lk, k1b, k2b, o_r, nxt - 1u - l);
         const uint32_t qx = scan_xor(v);
-        const uint64_t below = resm & ((uint64_t(1) << l) - 1u);
-        const uint32_t prv = below ? 63u - static_cast<uint32_t>(__builtin_clzll(below)) : 0u;
-        const uint32_t q1 = bperm(qx, l == 0u ? 0u : l - 1u);
-        const uint32_t q2 = bperm(qx, prv == 0u ? 0u : prv - 1u);
-        const uint32_t in_l = (l == 0u ? 0u : q1) ^ (prv == 0u ? 0u : q2);
+        {  // desk lanes whose span was cut here (stripe L = cs, reset stripe
+           // R): IN = q[L - 1] ^ q[R - 1], F from stripe L -- one exchange
+          const uint64_t below = resm & ((uint64_t(1) << cs) - 1u);
+          const uint32_t R = below ? 63u - static_cast<uint32_t>(__builtin_clzll(below)) : 0u;
+          const uint32_t g1 = bperm(qx, cut && cs != 0u ? cs - 1u : l);
+          const uint32_t g2 = bperm(qx, cut && R != 0u ? R - 1u : l);
+          const uint32_t gf = bperm(fr, cut ? cs : l);
+          if (cut) {
+            in_r = (cs == 0u ? 0u : g1) ^ (R == 0u ? 0u : g2);
+            f_r = gf;
+          }
+        }
         {  // the carry: the span open at the page's end, from its reset
            // stripe (a cut after the last reset: no span is open)
           const uint32_t plast = resm ? 63u - static_cast<uint32_t>(__builtin_clzll(resm)) : 0u;
           const uint32_t q63 = rdlane(qx, 63);
           const uint32_t qp = plast == 0u ? 0u : rdlane(qx, plast - 1u);
           carry = q63 ^ qp;
-        }
-        {  // desk lanes whose span was cut here take IN and F from the cut stripe
-          const uint32_t sl = cut ? cs : l;
-          const uint32_t gi = bperm(in_l, sl), gf = bperm(fr, sl);
-          if (cut) {
-            in_r = gi;
-            f_r = gf;
-          }
         }
         LP_ACC(5, 1);
 #if defined(WIPDB_LP_PROF) && !defined(WIPDB_LK_EMU)
