@@ -105,8 +105,11 @@ extern "C" {
  * NUMBER of spans.  For large batches of mixed sizes (config 3's Zipf mix:
  * the default deal leaves the busiest of 256 workgroups ~1.17x the mean);
  * same results, two extra launches and (G + 1) * 4 + 8 * n / 1024 bytes of
- * stream-ordered scratch.  Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG
- * and for batches of fewer than 64 spans per workgroup. */
+ * stream-ordered scratch.  Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG,
+ * for batches of fewer than 64 spans per workgroup, and on host pointers
+ * (hcrc_batch without HCRC_DEVICE_PTRS: those batches are bound by the
+ * host-device copy or the zero-copy reads, not by the kernel's balance, and
+ * the passes would only add two launches per staged piece). */
 #define HCRC_BALANCE 0x10
 /* SST-packed device batch (hcrc_batch_async / hcrc_batch with
  * HCRC_DEVICE_PTRS): the caller says the spans are sorted by offset, do not
@@ -117,9 +120,12 @@ extern "C" {
  * share of the bytes (stream-tiled kernel).  A small
  * pre-pass checks the promise (and that no 4 KiB holds more than 62 span
  * starts); a batch that breaks it runs the default pipeline instead, so
- * the flag can cost speed, never a CRC.  Scratch: (32 G + 9) * 4 bytes,
- * stream-ordered.  Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG;
- * HCRC_BALANCE is implied. */
+ * the flag can cost speed, never a CRC; a batch the default pipeline's
+ * end-aligned loop suits (aligned 4 KiB blocks, table blocks, spans of >= 16
+ * KiB) runs that loop.  Scratch: (16 G + 9) * 4 bytes, stream-ordered.
+ * Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG; HCRC_BALANCE is implied.
+ * On host pointers it applies to the device-side layout of each piece
+ * (staged pieces are packed by construction). */
 #define HCRC_PACKED 0x20
 
 typedef struct hcrc_ctx hcrc_ctx;

@@ -830,6 +830,44 @@ def test_packed_promise_broken_falls_back(engine, oracle):
         np.testing.assert_array_equal(got, oracle.batch(host, o, ln))
 
 
+def test_sync_batch_balance_and_packed_flags(engine, oracle):
+    """the synchronous hcrc_batch with HCRC_BALANCE and
+    HCRC_PACKED -- device pointers (HCRC_DEVICE_PTRS: the passes and the
+    pre-pass run) and host pointers (HCRC_BALANCE dropped, HCRC_PACKED on the
+    staged pieces' own layout) -- against the oracle, with inits and the
+    masked output."""
+    import ctypes
+    import torch
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(77)
+    offs, lens = _packed_layout(rng, 40000, 200, 3000, 5, 5, 3)
+    inits = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 16, dtype=np.uint8)
+    want = oracle.batch(host, offs, lens, inits)
+    want_m = oracle.batch(host, offs, lens, inits, mask=True)
+    d = torch.from_numpy(host).cuda()
+    do, dl, di = _t(offs), _t(lens), _t(inits)
+    for extra in (_lib.HCRC_BALANCE, _lib.HCRC_PACKED, _lib.HCRC_BALANCE | _lib.HCRC_PACKED):
+        for mask, ref in ((0, want), (_lib.HCRC_MASK_OUTPUT, want_m)):
+            out = torch.empty(lens.size, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            rc = lib.hcrc_batch(engine._ctx, ctypes.c_void_p(d.data_ptr()),
+                                ctypes.c_void_p(do.data_ptr()), ctypes.c_void_p(dl.data_ptr()),
+                                ctypes.c_void_p(di.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                lens.size, _lib.HCRC_DEVICE_PTRS | extra | mask)
+            assert rc == _lib.HCRC_OK, (extra, mask, rc)
+            np.testing.assert_array_equal(_u32(out), ref)
+            hout = np.empty(lens.size, np.uint32)
+            rc = lib.hcrc_batch(engine._ctx, host.ctypes.data_as(ctypes.c_void_p),
+                                offs.ctypes.data_as(ctypes.c_void_p),
+                                lens.ctypes.data_as(ctypes.c_void_p),
+                                inits.ctypes.data_as(ctypes.c_void_p),
+                                hout.ctypes.data_as(ctypes.c_void_p), lens.size, extra | mask)
+            assert rc == _lib.HCRC_OK, (extra, mask, rc)
+            np.testing.assert_array_equal(hout, ref)
+
+
 def test_packed_stream_only_matches_default():
     """The packed kernel hands batches that suit run_ea (aligned 4 KiB blocks,
     table blocks, spans of >= 16 KiB) to it; with WIPDB_PS_ONLY=1 run_ps takes

@@ -1169,8 +1169,10 @@ int hcrc_batch(hcrc_ctx* ctx, const void* base, const uint64_t* offsets, const u
     if (rc) return rc;
     return lane.CheckFaults();
   }
+  // host pointers: HCRC_BALANCE is dropped (the header: the copy or the
+  // zero-copy reads bound these batches, not the kernel's balance)
   return BatchHostLong(ctx, static_cast<const uint8_t*>(base), offsets, lengths, init_crcs,
-                       out_crcs, count, flags);
+                       out_crcs, count, flags & ~HCRC_BALANCE);
 }
 
 int hcrc_batch_async(hcrc_ctx* ctx, const void* d_base, const uint64_t* d_offsets,
