@@ -59,10 +59,14 @@ def dev(a, d):
 PRECONDITION_S = 0.08  # bench.py's power-transient preconditioning
 
 
-def time_kernel(fn, stream, reps):
-    """Average launch time of fn on `stream`, after untimed launches worth
-    PRECONDITION_S of GPU time (the first ~30-60 ms of back-to-back launches
-    after idle run slow while the SMU settles the clocks, bench.py)."""
+def time_kernel(fn, stream, reps, windows=2):
+    """Average launch time of fn on `stream` over `reps` back-to-back
+    launches, the best of `windows` such windows, after untimed launches
+    worth PRECONDITION_S of GPU time (the first ~30-60 ms of back-to-back
+    launches after idle run slow while the SMU settles the clocks, bench.py;
+    a single window right after a large allocation and fill once read 26 %
+    slow on a box that timed the same batch at its usual rate again a minute
+    later, profiles/r05z_bench.log vs r05z_tbl.log)."""
     fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -70,13 +74,17 @@ def time_kernel(fn, stream, reps):
         for _ in range(4):
             fn()
         torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record(stream)
-    for _ in range(reps):
-        fn()
-    e.record(stream)
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / reps / 1e3
+    best = None
+    for _ in range(max(1, windows)):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(reps):
+            fn()
+        e.record(stream)
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / reps / 1e3
+        best = t if best is None else min(best, t)
+    return best
 
 
 def usable_cpus() -> int:
