@@ -83,6 +83,7 @@ constexpr uint32_t kPsMinStream = 96;   // spans shorter than this are computed 
                                         // (a stream span's stream part is then >= 64 bytes)
 constexpr uint32_t kPsMaxGap = 4096;    // a larger gap could leave a page of no span's bytes
 constexpr uint32_t kPsDense = 62;       // spans i, i + 62 start >= 4 KiB apart
+constexpr uint32_t kPsDenseBytes = 1600;  // a desk of spans shorter on average plans a page ahead
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -165,12 +166,15 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
 // A page's events to the lanes of their stripes: the lanes with `ev`
 // (consecutive: the desk's stream spans in rank order, below) each hand
 // `val` (nonzero) to lane `stripe` (distinct, increasing with the lane);
-// the others get 0.  One or two
-// events: readlane / writelane; more: the OR of the stripe bits (DPP), each
-// stripe lane's rank among them (mbcnt) and one ds_bpermute from its desk
-// lane -- a fixed cost, where the per-event chain is a few hundred cycles
-// of dependent scalar / vector hand-offs per event.
-__device__ __forceinline__ uint32_t ps_deliver(uint32_t l, bool ev, uint32_t stripe, uint32_t val) {
+// the others get 0.  The OR of the event stripes (DPP), each stripe lane's
+// rank among them (mbcnt) and one ds_bpermute: no branch, so the page loop
+// runs it for the next page inside this page's scan (a latency chain beside
+// another).
+// The same for pages of few events (desks of long spans): v_writelane for one
+// or two, the general form for more -- cheaper per page, but a branch, so
+// it runs in the page's own turn, not inside the previous page's scan.
+__device__ __forceinline__ uint32_t ps_deliver(uint32_t l, bool ev, uint32_t stripe, uint32_t val);
+__device__ __forceinline__ uint32_t ps_deliver_few(uint32_t l, bool ev, uint32_t stripe, uint32_t val) {
   const uint64_t m = ballot(ev);
   if (m == 0u) return 0u;
   if (__builtin_popcountll(m) <= 2) {
@@ -181,10 +185,14 @@ __device__ __forceinline__ uint32_t ps_deliver(uint32_t l, bool ev, uint32_t str
     }
     return r;
   }
+  return ps_deliver(l, ev, stripe, val);
+}
+__device__ __forceinline__ uint32_t ps_deliver(uint32_t l, bool ev, uint32_t stripe, uint32_t val) {
+  const uint64_t m = ballot(ev);
   const uint32_t lo = scan_or(ev && stripe < 32u ? 1u << stripe : 0u);
   const uint32_t hi = scan_or(ev && stripe >= 32u ? 1u << (stripe - 32u) : 0u);
   const uint32_t k = mbcnt_hi(hi, mbcnt_lo(lo, 0u));  // event stripes below the lane
-  const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(m)) + k;
+  const uint32_t j = (m != 0u ? static_cast<uint32_t>(__builtin_ctzll(m)) : 0u) + k;
   const uint32_t v = bperm(val, j & 63u);
   const bool mine = ((l < 32u ? lo >> l : hi >> (l - 32u)) & 1u) != 0u;
   return mine ? v : 0u;
@@ -378,16 +386,34 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           last_desk ? wend : umin(wend, uni(rdlane(a32, dn - 1u)) & ~4095u);
       LP_T(dk1);
       LP_ACC(3, dk1 - dk0);
+      // a page's events to their stripes' lanes (rz: reset before chunk
+      // rz - 1, 0 = none; tc: cut after chunk tc - 1, 0 = none).  A desk of
+      // short spans (many events a page) plans each next page inside the
+      // page before (the branch-free form, its latency beside the scan's);
+      // one of long spans plans each page in its own turn (v_writelane)
+      const bool dense =
+          uni(rdlane(b32, dn - 1u)) - uni(rdlane(a32, 0u)) < dn * kPsDenseBytes;
+      auto page_loop = [&](auto kDense) {
+      constexpr bool D = decltype(kDense)::value;
+      auto plan = [&](uint32_t wi, uint32_t& tcp, uint32_t& rzp) {
+        if constexpr (D) {
+          tcp = ps_deliver(l, cev != ~0u && (cev >> 12) == wi, (cev >> 3) & 63u, cev & 7u);
+          rzp = ps_deliver(l, hev != ~0u && (hev >> 12) == wi, (hev >> 3) & 63u, hev & 7u);
+        } else {
+          tcp = ps_deliver_few(l, cev != ~0u && (cev >> 12) == wi, (cev >> 3) & 63u, cev & 7u);
+          rzp = ps_deliver_few(l, hev != ~0u && (hev >> 12) == wi, (hev >> 3) & 63u, hev & 7u);
+        }
+      };
+      uint32_t tc_n = 0, rz_n = 0;
+      if constexpr (D) plan(wr >> 12, tc_n, rz_n);
       for (; wr < wstop; wr += 4096u, ++pages) {
-        // ---- the page's events, planned before it lands: resets and cuts
-        // to their stripes' lanes (rz: reset before chunk rz - 1, 0 = none;
-        // tc: cut after chunk tc - 1, 0 = none) ----
+        // ---- the page's events (a dense desk planned them a page ahead) ----
         LP_T(p0);
         const uint32_t wi = wr >> 12;
         const bool head = hwin == wi;
         const bool cut = cwin == wi;
-        const uint32_t tc = ps_deliver(l, cev != ~0u && (cev >> 12) == wi, (cev >> 3) & 63u, cev & 7u);
-        const uint32_t rz = ps_deliver(l, hev != ~0u && (hev >> 12) == wi, (hev >> 3) & 63u, hev & 7u);
+        if constexpr (!D) plan(wi, tc_n, rz_n);
+        const uint32_t tc = tc_n, rz = rz_n;
         LP_T(w0);
         LP_ACC(6, w0 - p0);
         wait_vm<0>();
@@ -435,6 +461,7 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           // no span ends in this page but at its end (aligned blocks) and
           // none starts but at its start: the plain scan and the whole-page
           // fold give the open span's register at the page's end
+          if constexpr (D) plan(wi + 1u, tc_n, rz_n);
           const uint32_t r = fold<1>(lk, l, scan(lk, W))[0];
           carry = at_end ? 0u : r;
           if (at_end && cut) {
@@ -448,6 +475,7 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
 #endif
           continue;
         }
+        if constexpr (D) plan(wi + 1u, tc_n, rz_n);
         uint32_t x = W[0], fr = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -498,6 +526,9 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         LP_ACC(2, w3 - w2);
 #endif
       }
+      };
+      if (dense) page_loop(std::true_type{});
+      else page_loop(std::false_type{});
       if (wr >= wend) break;
       // ---- the next desk: the spans done are a prefix (ordered spans): a
       // stream span once its cut is behind the page, any other once its
