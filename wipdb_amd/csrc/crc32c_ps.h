@@ -287,6 +287,15 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
     bool last_desk = false;
     uint32_t carry = 0;
     uint32_t wr = 0;
+    // a desk's descriptors, loaded ahead: the first desk's here (behind the
+    // first page's DMA), each next one's before the previous desk's
+    // deferred span ends run
+    uint64_t nx_a = 0;
+    uint32_t nx_n = 0, nx_iv = 0;
+    auto load_desc = [&]() {
+      if (l < umin(kPsDesk, s_hi - d0)) src.lane(d0 + l, nx_a, nx_n, nx_iv);
+    };
+    load_desc();
 
     // the deferred end of the stream spans of the desk whose cut is done
     // (lanes in `done`): R = IN * x^(32 t) ^ F (t = 4 tc words), the tail's
@@ -303,12 +312,18 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       }
       r ^= f_r;
       const uint32_t k16 = b32 & 15u, kw = k16 >> 2;
-      const uint32_t t0 = step(lk, r ^ tt.x, 0u);
-      r = kw >= 1u ? t0 : r;
-      const uint32_t t1 = step(lk, r ^ tt.y, 0u);
-      r = kw >= 2u ? t1 : r;
-      const uint32_t t2 = step(lk, r ^ tt.z, 0u);
-      r = kw >= 3u ? t2 : r;
+      if (ballot(me && kw >= 1u) != 0u) {
+        const uint32_t t0 = step(lk, r ^ tt.x, 0u);
+        r = kw >= 1u ? t0 : r;
+      }
+      if (ballot(me && kw >= 2u) != 0u) {
+        const uint32_t t1 = step(lk, r ^ tt.y, 0u);
+        r = kw >= 2u ? t1 : r;
+      }
+      if (ballot(me && kw >= 3u) != 0u) {
+        const uint32_t t2 = step(lk, r ^ tt.z, 0u);
+        r = kw >= 3u ? t2 : r;
+      }
       const uint32_t twd = kw == 0u ? tt.x : (kw == 1u ? tt.y : (kw == 2u ? tt.z : tt.w));
       r = tail_step(lk, r, twd, k16 & 3u);
       const uint32_t crc = ~r;
@@ -322,13 +337,12 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       last_desk = d0 + dn == s_hi;
       {
         const bool v = l < dn;
-        uint64_t a = 0;
-        uint32_t n = 0, iv = 0;
-        if (v) src.lane(d0 + l, a, n, iv);
         wait_vm<0>();
-        loads_landed(a);
-        loads_landed(n);
-        loads_landed(iv);
+        loads_landed(nx_a);
+        loads_landed(nx_n);
+        loads_landed(nx_iv);
+        const uint64_t a = v ? nx_a : 0u;
+        const uint32_t n = v ? nx_n : 0u, iv = v ? nx_iv : 0u;
         a32 = v ? static_cast<uint32_t>(sbase + a - W0) : wend;
         b32 = v ? a32 + n : wend;
         id = d0 + l;
@@ -535,15 +549,16 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
       // bytes are (answered at its desk's load) ----
       const bool done = l < dn && (sstream ? (b32 & ~15u) <= wr : b32 <= wr);
       const uint32_t ngone = static_cast<uint32_t>(__builtin_popcountll(ballot(done)));
-      LP_T(f0);
-      finish(ballot(done && sstream));
-      LP_T(f1);
-      LP_ACC(8, f1 - f0);
       if (ngone == 0u) {  // (cannot happen in a checked batch: at most 63 spans meet a page)
         report_fault(fault, kFaultPsDesk);
         return;
       }
       d0 += ngone;
+      load_desc();  // the next desk's descriptors, behind the deferred ends
+      LP_T(f0);
+      finish(ballot(done && sstream));
+      LP_T(f1);
+      LP_ACC(8, f1 - f0);
     }
     // ---- the chunk's end: every stream span of its last desk ----
     LP_T(f0);
