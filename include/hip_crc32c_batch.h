@@ -125,7 +125,9 @@ extern "C" {
  * KiB) runs that loop.  Scratch: (16 G + 9) * 4 bytes, stream-ordered.
  * Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG; HCRC_BALANCE is implied.
  * On host pointers it applies to the device-side layout of each piece
- * (staged pieces are packed by construction). */
+ * (staged pieces are packed by construction).  A launch of fewer than 32 Ki
+ * spans runs the default path: the pre-pass costs ~10 us a call, which the
+ * stream repays only on batches of more than ~128 MiB of short spans. */
 #define HCRC_PACKED 0x20
 
 typedef struct hcrc_ctx hcrc_ctx;

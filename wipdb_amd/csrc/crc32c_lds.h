@@ -98,9 +98,6 @@ WIPDB_LK_HD constexpr uint32_t SegAuxAddr(uint32_t w) { return kLdsL2 + (128u + 
 
 // Flags of a launch (the HCRC_MASK_OUTPUT value is shared with the C-ABI).
 constexpr uint32_t kFlagMask = 0x2;
-// run_ps: workgroup g takes chunks g, g + G, g + 2G, ... (round robin)
-// instead of the contiguous range [C g / G, C (g + 1) / G)
-constexpr uint32_t kFlagPsRR = 0x100;
 // the packed kernel: run_ps even where run_ea suits the batch (tests, A/Bs)
 constexpr uint32_t kFlagPsOnly = 0x200;
 // Fault bits a launch ORs into its error word (a span was left uncomputed;

@@ -88,17 +88,6 @@ constexpr uint32_t kPsDenseBytes = 1600;  // a desk of spans shorter on average 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-// the inclusive max over lanes 0 .. l (values >= 0; lanes without a DPP
-// source read 0)
-__device__ __forceinline__ uint32_t scan_max(uint32_t v) {
-  v = umax(v, dpp<0x111>(v));
-  v = umax(v, dpp<0x112>(v));
-  v = umax(v, dpp<0x114>(v));
-  v = umax(v, dpp<0x118>(v));
-  v = umax(v, bcast15(v));
-  return umax(v, bcast31(v));
-}
-
 // The LDS address of window byte p (< 4096) in a wave slot: the window DMA
 // (Pipe::cm) puts window chunk 64 q + cm(m) at slot + 1024 q + 16 m, so the
 // lanes' stripe reads are conflict-free; m = cm^-1(c).
@@ -208,10 +197,8 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
   const uint32_t l = lane_tid() & 63u;
   const uint32_t w = uni(lane_tid() >> 6);
   const uint32_t G = group_count(), g = group_id();
-  const bool rr = (flags & kFlagPsRR) != 0u;
-  const uint32_t c_lo = rr ? 0u : static_cast<uint32_t>(static_cast<uint64_t>(C) * g / G);
-  const uint32_t c_hi = rr ? (C > g ? (C - g + G - 1u) / G : 0u)
-                           : static_cast<uint32_t>(static_cast<uint64_t>(C) * (g + 1u) / G);
+  const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(C) * g / G);
+  const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(C) * (g + 1u) / G);
   if (c_lo >= c_hi) return;
   // the wave's progress word (pages done), read by the others (below)
   const uint32_t prog_addr = MiscAddr(kMiscPsProgress + w);
@@ -272,7 +259,6 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
     if (l == 0u) cc = lds_add(MiscAddr(kMiscUnit), 1u);
     cc = uni(cc) + c_lo;
     if (cc >= c_hi) break;
-    if (rr) cc = cc * G + g;
     const uint32_t s_lo = uni(first[cc]), s_hi = uni(first[cc + 1u]);
     if (s_lo >= s_hi) continue;
     LP_ACC(9, 1);

@@ -517,6 +517,8 @@ int LaunchLong(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const ui
 // piece's lengths are known: it takes the split only when one of its spans
 // is long enough to be cut (AutoLongHost).
 constexpr size_t kAutoLongSpans = 16;
+// HCRC_PACKED launches of fewer spans run the default path (LaunchSpans)
+constexpr size_t kPackedMinSpans = size_t(1) << 15;
 enum class AutoLong { kNo, kDevice };
 
 #ifdef WIPDB_HCRC_TEST_HOOKS
@@ -593,7 +595,14 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                          init ? init + pos : nullptr, out + pos, n, 0, mask, st);
     } else {
       const int grid = LdsGrid(ctx, n);
-      if (flags & HCRC_PACKED) {
+      // (HCRC_PACKED on fewer than kPackedMinSpans spans: the default path --
+      // the pre-pass's launches cost ~10 us a call, more than the stream
+      // saves on batches below ~128 MiB, profiles/r05ae_latency*.log)
+      static const size_t packed_min = [] {
+        const char* e = getenv("WIPDB_PS_MIN_SPANS");
+        return e && *e ? static_cast<size_t>(atol(e)) : kPackedMinSpans;
+      }();
+      if ((flags & HCRC_PACKED) && n >= packed_min) {
         // HCRC_PACKED: the pre-pass checks the batch and cuts its covering
         // range into C equal byte chunks (first[c]); the packed kernel then
         // streams it (crc32c_ps.h), or runs the default pipeline when the
@@ -603,7 +612,6 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
           const int v = e ? atoi(e) : 0;
           return v >= 1 && v <= 1024 ? v : 16;  // one chunk per wave (progress-balanced)
         }();
-        static const bool ps_rr = getenv("WIPDB_PS_RR") && atoi(getenv("WIPDB_PS_RR")) != 0;
         // (tests, A/Bs: the stream-tiled pipeline even where run_ea suits the batch)
         static const bool ps_only = getenv("WIPDB_PS_ONLY") && atoi(getenv("WIPDB_PS_ONLY")) != 0;
         const uint32_t C = static_cast<uint32_t>(chunks_per_group * grid);
@@ -629,7 +637,7 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                            dim3(grid), dim3(lk::kThreads), lk::kLdsBytes, st,
                            static_cast<const uint8_t*>(base), off + pos, len + pos,
                            init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n),
-                           (mask ? lk::kFlagMask : 0u) | (ps_rr ? lk::kFlagPsRR : 0u) |
+                           (mask ? lk::kFlagMask : 0u) |
                                (ps_only ? lk::kFlagPsOnly : 0u),
                            ctx->d_image, first, meta, C, fault);
         rc = LaunchedLp(st, fault);
