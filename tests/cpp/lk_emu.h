@@ -175,6 +175,11 @@ inline void loads_landed(T&) {}
 inline uint32_t vzero() { return 0u; }
 
 inline void global_or(uint32_t* a, uint32_t v) { __atomic_fetch_or(a, v, __ATOMIC_SEQ_CST); }
+inline void global_max(uint32_t* a, uint32_t v) {
+  uint32_t c = __atomic_load_n(a, __ATOMIC_SEQ_CST);
+  while (c < v && !__atomic_compare_exchange_n(a, &c, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
+  }
+}
 
 // ---- faults ----
 // the fault bits of the launches (the device counts faulting waves instead)

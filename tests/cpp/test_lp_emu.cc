@@ -319,12 +319,16 @@ void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std:
     const uint32_t c = Extend(inits ? (*inits)[i] : 0u, data + offs[i], lens[i]);
     want[i] = mask ? wipdb::gf2::Mask(c) : c;
   }
+  // the verdict word as a stream's earlier launches left it (an older
+  // epoch's tag, broken): the pre-pass must raise it to this launch's
+  constexpr uint32_t kEpoch = 7;
   std::vector<uint32_t> first(C + 1, 0xFFFFFFFFu), meta(kPsMetaWords, 0u);
+  meta[0] = (kEpoch - 1) << 4 | kPsBad;
   const uint32_t pgrid = static_cast<uint32_t>(std::min<size_t>((n + 255) / 256, 8));
   emu::launch(pgrid ? pgrid : 1, [&] {
-    crc32c_ps_index_kernel(offs.data(), lens.data(), n, C, first.data(), meta.data());
+    crc32c_ps_index_kernel(offs.data(), lens.data(), n, C, first.data(), meta.data(), kEpoch);
   });
-  const bool packed = meta[0] == 0u;
+  const bool packed = meta[0] == kEpoch << 4;
   if (packed)
     for (uint32_t c = 0; c <= C; ++c)
       if (first[c] > n || (c && first[c] < first[c - 1])) {
@@ -341,11 +345,11 @@ void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std:
     if (inits)
       crc32c_lds_packed_kernel<1>(data, offs.data(), lens.data(), inits->data(), got.data(), n,
                                   (mask ? kFlagMask : 0u) | g_packed_flags, img, first.data(), meta.data(), C,
-                                  &g_fault_word);
+                                  kEpoch, &g_fault_word);
     else
       crc32c_lds_packed_kernel<0>(data, offs.data(), lens.data(), nullptr, got.data(), n,
                                   (mask ? kFlagMask : 0u) | g_packed_flags, img, first.data(), meta.data(), C,
-                                  &g_fault_word);
+                                  kEpoch, &g_fault_word);
   });
   char label[96];
   const int pipes = emu::g_pipes.load();

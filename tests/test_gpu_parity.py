@@ -935,6 +935,7 @@ def test_packed_prepass_verdicts():
         "o4 = o.copy(); o4[700:] += 5000\n"
         "cases['gap5k'] = (o4, l)\n"
         "cases['dense'] = lay(20000, 5, 60, 7)\n"
+        "cases['again'] = cases['512-2k']\n"
         "res = {}\n"
         "with Engine(0) as eng:\n"
         "    size = max(int((o + l).max()) for o, l in cases.values()) + 64\n"
@@ -956,7 +957,9 @@ def test_packed_prepass_verdicts():
     import json
     res = json.loads(r.stdout.split("META ", 1)[1].splitlines()[0])
     print(res)
-    for k in ("512-2k", "tblocks", "a4k", "b65536", "shorts"):
+    # ("again": a packed batch after four broken ones on the same lanes:
+    # each launch's verdict is its own, not a leftover)
+    for k in ("512-2k", "tblocks", "a4k", "b65536", "shorts", "again"):
         assert res[k][0] == 0, (k, res[k])
         assert res[k][1] % 4096 == 0 and res[k][1] >= 4096, (k, res[k])
     for k in ("unsorted", "overlap", "gap5k"):

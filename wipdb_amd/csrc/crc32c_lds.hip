@@ -1068,41 +1068,44 @@ template __global__ void crc32c_lds_spans_kernel<1>(const uint8_t*, const uint64
 // Packed batch (HCRC_PACKED, crc32c_ps.h): run_ea when the batch suits it
 // (pick_ea: aligned 4 KiB blocks, table blocks, spans of >= 16 KiB -- where it
 // is 4-7 % faster than run_ps, profiles/r05v_ab.log), else run_ps when the
-// pre-pass found the batch packed (meta[0] == 0), else the lane-packed
-// pipeline -- a broken promise costs speed, never a CRC.  first / C: the
-// chunk index.
+// pre-pass found the batch packed (meta[0] == epoch << 4: this launch's
+// verdict, nothing broken), else the lane-packed pipeline -- a broken
+// promise (or a verdict that is not this launch's) costs speed, never a
+// CRC.  first / C: the chunk index.
 template <int INIT>
 __global__ __launch_bounds__(kThreads) void crc32c_lds_packed_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image,
     const uint32_t* __restrict__ first, const uint32_t* __restrict__ meta, uint32_t C,
-    unsigned int* fault) {
+    uint32_t epoch, unsigned int* fault) {
   const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u, nullptr};
   if ((flags & kFlagPsOnly) == 0u && pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
-  else if (meta[0] != 0u) run_lp<0>(src, out, flags & kFlagMask, image, fault);
+  else if (meta[0] != epoch << 4) run_lp<0>(src, out, flags & kFlagMask, image, fault);
   else run_ps(src, out, flags, image, first, C, fault);
 }
 template __global__ void crc32c_lds_packed_kernel<0>(const uint8_t*, const uint64_t*,
                                                      const uint32_t*, const uint32_t*, uint32_t*,
                                                      uint64_t, uint32_t, const uint8_t*,
                                                      const uint32_t*, const uint32_t*, uint32_t,
-                                                     unsigned int*);
+                                                     uint32_t, unsigned int*);
 template __global__ void crc32c_lds_packed_kernel<1>(const uint8_t*, const uint64_t*,
                                                      const uint32_t*, const uint32_t*, uint32_t*,
                                                      uint64_t, uint32_t, const uint8_t*,
                                                      const uint32_t*, const uint32_t*, uint32_t,
-                                                     unsigned int*);
+                                                     uint32_t, unsigned int*);
 
-// The packed batch's pre-pass (crc32c_ps.h ps_index): meta zeroed by the host.
+// The packed batch's pre-pass (crc32c_ps.h ps_index); epoch: the launch's
+// tag of the verdict word (1 .. 2^28 - 1, the host's per-stream count).
 __global__ __launch_bounds__(256) void crc32c_ps_index_kernel(const uint64_t* __restrict__ offsets,
                                                               const uint32_t* __restrict__ lengths,
                                                               uint64_t count, uint32_t C,
                                                               uint32_t* __restrict__ first,
-                                                              uint32_t* __restrict__ meta) {
+                                                              uint32_t* __restrict__ meta,
+                                                              uint32_t epoch) {
   const uint64_t nt = static_cast<uint64_t>(group_count()) * 256u;
   const uint64_t tid = static_cast<uint64_t>(group_id()) * 256u + (lane_tid() & 255u);
-  ps_index(nullptr, offsets, lengths, count, C, first, meta, tid, nt);
+  ps_index(nullptr, offsets, lengths, count, C, first, meta, tid, nt, epoch);
 }
 
 // Fixed-size blocks at a fixed stride.

@@ -72,6 +72,10 @@ __device__ __forceinline__ uint32_t vzero() { return __builtin_amdgcn_mbcnt_lo(0
 __device__ __forceinline__ void global_or(uint32_t* a, uint32_t v) {
   __hip_atomic_fetch_or(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a = max(a, v) in global memory (agent scope; the epoch-tagged verdict)
+__device__ __forceinline__ void global_max(uint32_t* a, uint32_t v) {
+  __hip_atomic_fetch_max(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---- faults ----
 // A queue record's marker as read (the host emulation can hide one to force

@@ -104,13 +104,17 @@ __device__ __forceinline__ uint32_t low_bytes(uint32_t b) {
 
 // ---------------------------------------------------------------------------
 // The pre-pass: check the batch, cut its covering range into C chunks.
-// Thread i handles span i (grid-stride); meta[0] is ORed, first[] written
-// where the chunk index steps.  first has C + 1 entries, first[C] = n.
+// Thread i handles span i (grid-stride); first[] written where the chunk
+// index steps (first has C + 1 entries, first[C] = n).  The verdict word
+// meta[0] is tagged with the launch's epoch (its stream's count of packed
+// launches): thread 0 raises it to epoch << 4, a thread that finds the
+// batch broken to epoch << 4 | kPsBad*, so it needs no clearing between
+// launches (a stale word is an older epoch, lower).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* off,
                                          const uint32_t* len, uint64_t n, uint32_t C,
                                          uint32_t* first, uint32_t* meta, uint64_t tid,
-                                         uint64_t nthreads) {
+                                         uint64_t nthreads, uint32_t epoch) {
   if (n == 0) return;
   const uint64_t lo = off[0];
   const uint64_t hi = off[n - 1] + len[n - 1];
@@ -149,7 +153,7 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
       for (uint64_t k = c + 1u; k <= C; ++k) first[k] = static_cast<uint32_t>(n);
   }
   (void)base;
-  if (bad) global_or(meta, bad);
+  if (tid == 0 || bad) global_max(meta, (epoch << 4) | bad);
 }
 
 // A page's events to the lanes of their stripes: the lanes with `ev`

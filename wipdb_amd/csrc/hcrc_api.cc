@@ -48,9 +48,9 @@ template <int INIT>
 __global__ void crc32c_lds_packed_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                          const uint32_t*, uint32_t*, uint64_t, uint32_t,
                                          const uint8_t*, const uint32_t*, const uint32_t*, uint32_t,
-                                         unsigned int*);
+                                         uint32_t, unsigned int*);
 __global__ void crc32c_ps_index_kernel(const uint64_t*, const uint32_t*, uint64_t, uint32_t,
-                                       uint32_t*, uint32_t*);
+                                       uint32_t*, uint32_t*, uint32_t);
 template <int G, int OUT>
 __global__ void crc32c_lds_list_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                        const uint32_t*, const uint32_t*, const uint32_t*, void*,
@@ -288,6 +288,16 @@ struct hcrc_ctx {
   unsigned int* d_fault_words = nullptr;
   std::mutex faults_mu;
   std::map<hipStream_t, uint32_t> stream_words;
+  // HCRC_PACKED's pre-pass output per stream (meta words + the chunk index),
+  // kept across launches: the verdict word is tagged with the stream's
+  // launch count, so nothing is cleared or allocated per call
+  struct PsScratch {
+    uint32_t* d = nullptr;
+    uint32_t epoch = 0;
+    std::mutex mu;  // a launch pair (pre-pass, kernel) is enqueued whole
+  };
+  std::mutex ps_mu;
+  std::map<hipStream_t, std::unique_ptr<PsScratch>> ps_scratch;
   // lanes of synchronous calls
   std::mutex lanes_mu;
   std::condition_variable lanes_cv;
@@ -570,6 +580,23 @@ unsigned int* StreamFaultWord(hcrc_ctx* ctx, hipStream_t st) {
   return ctx->d_fault_words + k;
 }
 
+// The stream's HCRC_PACKED scratch (words 32-bit words, cleared once),
+// created on the stream's first packed launch; nullptr when out of memory.
+hcrc_ctx::PsScratch* PsScratchFor(hcrc_ctx* ctx, hipStream_t st, size_t words) {
+  std::lock_guard<std::mutex> lk(ctx->ps_mu);
+  auto it = ctx->ps_scratch.find(st);
+  if (it != ctx->ps_scratch.end()) return it->second.get();
+  auto ps = std::make_unique<hcrc_ctx::PsScratch>();
+  if (hipMalloc(reinterpret_cast<void**>(&ps->d), words * 4) != hipSuccess) return nullptr;
+  if (hipMemset(ps->d, 0, words * 4) != hipSuccess) {
+    (void)hipFree(ps->d);
+    return nullptr;
+  }
+  hcrc_ctx::PsScratch* raw = ps.get();
+  ctx->ps_scratch.emplace(st, std::move(ps));
+  return raw;
+}
+
 // Descriptor batch on device memory, enqueued on st.  auto_long: kDevice for
 // the device entry points (a batch of <= kAutoLongSpans spans splits its long
 // spans by itself); host pieces decide on the host (AutoLongHost).
@@ -615,23 +642,28 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         // (tests, A/Bs: the stream-tiled pipeline even where run_ea suits the batch)
         static const bool ps_only = getenv("WIPDB_PS_ONLY") && atoi(getenv("WIPDB_PS_ONLY")) != 0;
         const uint32_t C = static_cast<uint32_t>(chunks_per_group * grid);
-        const size_t bytes = (size_t(C) + 1 + lk::kPsMetaWords) * 4;
-        uint8_t* scratch = nullptr;
-        HCRC_CHECK(hipMallocFromPoolAsync(reinterpret_cast<void**>(&scratch), bytes,
-                                          ctx->scratch_pool, st));
-        uint32_t* meta = reinterpret_cast<uint32_t*>(scratch);
+        const size_t words = size_t(chunks_per_group) * ctx->num_cu + 1 + lk::kPsMetaWords;
+        hcrc_ctx::PsScratch* ps = PsScratchFor(ctx, st, words);
+        if (!ps) return HCRC_ERR_NO_MEMORY;
+        std::lock_guard<std::mutex> psl(ps->mu);
+        if (++ps->epoch >= (1u << 28)) {  // (the tag's range: start over from a cleared word)
+          HCRC_CHECK(hipMemsetAsync(ps->d, 0, lk::kPsMetaWords * 4, st));
+          ps->epoch = 1;
+        }
+        uint32_t* meta = ps->d;
         uint32_t* first = meta + lk::kPsMetaWords;
-        HCRC_CHECK(hipMemsetAsync(meta, 0, lk::kPsMetaWords * 4, st));
         const int pgrid = static_cast<int>(
             std::max<size_t>(1, std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8)));
         hipLaunchKernelGGL(lk::crc32c_ps_index_kernel, dim3(pgrid), dim3(256), 0, st, off + pos,
-                           len + pos, static_cast<uint64_t>(n), C, first, meta);
+                           len + pos, static_cast<uint64_t>(n), C, first, meta, ps->epoch);
 #ifdef WIPDB_HCRC_TEST_HOOKS
         // (test build: the pre-pass's verdict and chunk size, for the tests
-        // that check which pipeline a packed batch took)
+        // that check which pipeline a packed batch took; word 0 as the
+        // kernel reads it: 0 = this launch's and packed, else its bits)
         HCRC_CHECK(hipMemcpyAsync(g_test_ps_meta, meta, sizeof(g_test_ps_meta),
                                   hipMemcpyDeviceToHost, st));
         HCRC_CHECK(hipStreamSynchronize(st));
+        g_test_ps_meta[0] = (g_test_ps_meta[0] >> 4) == ps->epoch ? (g_test_ps_meta[0] & 15u) : ~0u;
 #endif
         hipLaunchKernelGGL(init ? lk::crc32c_lds_packed_kernel<1> : lk::crc32c_lds_packed_kernel<0>,
                            dim3(grid), dim3(lk::kThreads), lk::kLdsBytes, st,
@@ -639,9 +671,8 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                            init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n),
                            (mask ? lk::kFlagMask : 0u) |
                                (ps_only ? lk::kFlagPsOnly : 0u),
-                           ctx->d_image, first, meta, C, fault);
+                           ctx->d_image, first, meta, C, ps->epoch, fault);
         rc = LaunchedLp(st, fault);
-        if (hipFreeAsync(scratch, st) != hipSuccess && rc == HCRC_OK) rc = HCRC_ERR_HIP;
         if (rc) return rc;
         continue;
       }
@@ -1154,6 +1185,8 @@ hcrc_ctx::~hcrc_ctx() {
     (void)hipMemPoolDestroy(scratch_pool);
   }
   if (fault_words) (void)hipHostFree(fault_words);
+  for (auto& kv : ps_scratch)
+    if (kv.second->d) (void)hipFree(kv.second->d);
 }
 
 void* hcrc_ctx_stream(hcrc_ctx* ctx) { return ctx ? ctx->stream : nullptr; }
