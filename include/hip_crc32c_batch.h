@@ -122,7 +122,8 @@ extern "C" {
  * starts); a batch that breaks it runs the default pipeline instead, so
  * the flag can cost speed, never a CRC; a batch the default pipeline's
  * end-aligned loop suits (aligned 4 KiB blocks, table blocks, spans of >= 16
- * KiB) runs that loop.  Scratch: (16 G + 9) * 4 bytes, stream-ordered.
+ * KiB) runs that loop.  Scratch: (16 G + 9) * 4 bytes per stream that
+ * launches one, allocated on its first and kept with the context.
  * Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG; HCRC_BALANCE is implied.
  * On host pointers it applies to the device-side layout of each piece
  * (staged pieces are packed by construction).  A launch of fewer than 32 Ki
