@@ -676,6 +676,12 @@ int main(int argc, char** argv) {
                 true, 2, 0, true);
     }
     {
+      // two spans a page at most: the desks' two-event hand-off
+      auto l = lens_of(700, 1600, 2600);
+      RunPacked("packed 1.6..2.6 KiB", buf.data(), buf.size(), Packed(l, 9, 4), l, nullptr, false, 3, 0,
+                true);
+    }
+    {
       auto l = lens_of(500, 4097, 4225);
       RunPacked("packed table blocks", buf.data(), buf.size(), Packed(l, 0, 4), l, nullptr, true, 3, 0,
                 true);
