@@ -529,6 +529,9 @@ int LaunchLong(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* off, const ui
 constexpr size_t kAutoLongSpans = 16;
 // HCRC_PACKED launches of fewer spans run the default path (LaunchSpans)
 constexpr size_t kPackedMinSpans = size_t(1) << 15;
+// streams with a packed scratch of their own (~16 KiB each); further streams'
+// packed batches take the default path
+constexpr size_t kPsStreams = 1024;
 enum class AutoLong { kNo, kDevice };
 
 #ifdef WIPDB_HCRC_TEST_HOOKS
@@ -581,11 +584,13 @@ unsigned int* StreamFaultWord(hcrc_ctx* ctx, hipStream_t st) {
 }
 
 // The stream's HCRC_PACKED scratch (words 32-bit words, cleared once),
-// created on the stream's first packed launch; nullptr when out of memory.
+// created on the stream's first packed launch; nullptr past kPsStreams
+// streams or out of memory.
 hcrc_ctx::PsScratch* PsScratchFor(hcrc_ctx* ctx, hipStream_t st, size_t words) {
   std::lock_guard<std::mutex> lk(ctx->ps_mu);
   auto it = ctx->ps_scratch.find(st);
   if (it != ctx->ps_scratch.end()) return it->second.get();
+  if (ctx->ps_scratch.size() >= kPsStreams) return nullptr;
   auto ps = std::make_unique<hcrc_ctx::PsScratch>();
   if (hipMalloc(reinterpret_cast<void**>(&ps->d), words * 4) != hipSuccess) return nullptr;
   if (hipMemset(ps->d, 0, words * 4) != hipSuccess) {
@@ -629,22 +634,25 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         const char* e = getenv("WIPDB_PS_MIN_SPANS");
         return e && *e ? static_cast<size_t>(atol(e)) : kPackedMinSpans;
       }();
-      if ((flags & HCRC_PACKED) && n >= packed_min) {
+      static const int chunks_per_group = [] {
+        const char* e = getenv("WIPDB_PS_CHUNKS");  // (tuning: chunks per workgroup)
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 1024 ? v : 16;  // one chunk per wave (progress-balanced)
+      }();
+      // the stream's pre-pass scratch (none: past kPsStreams streams or out
+      // of memory -- the batch takes the default path)
+      hcrc_ctx::PsScratch* const ps =
+          (flags & HCRC_PACKED) && n >= packed_min
+              ? PsScratchFor(ctx, st, size_t(chunks_per_group) * ctx->num_cu + 1 + lk::kPsMetaWords)
+              : nullptr;
+      if (ps) {
         // HCRC_PACKED: the pre-pass checks the batch and cuts its covering
         // range into C equal byte chunks (first[c]); the packed kernel then
         // streams it (crc32c_ps.h), or runs the default pipeline when the
         // pre-pass found the batch not packed
-        static const int chunks_per_group = [] {
-          const char* e = getenv("WIPDB_PS_CHUNKS");  // (tuning: chunks per workgroup)
-          const int v = e ? atoi(e) : 0;
-          return v >= 1 && v <= 1024 ? v : 16;  // one chunk per wave (progress-balanced)
-        }();
         // (tests, A/Bs: the stream-tiled pipeline even where run_ea suits the batch)
         static const bool ps_only = getenv("WIPDB_PS_ONLY") && atoi(getenv("WIPDB_PS_ONLY")) != 0;
         const uint32_t C = static_cast<uint32_t>(chunks_per_group * grid);
-        const size_t words = size_t(chunks_per_group) * ctx->num_cu + 1 + lk::kPsMetaWords;
-        hcrc_ctx::PsScratch* ps = PsScratchFor(ctx, st, words);
-        if (!ps) return HCRC_ERR_NO_MEMORY;
         std::lock_guard<std::mutex> psl(ps->mu);
         if (++ps->epoch >= (1u << 28)) {  // (the tag's range: start over from a cleared word)
           HCRC_CHECK(hipMemsetAsync(ps->d, 0, lk::kPsMetaWords * 4, st));
