@@ -1507,6 +1507,60 @@ def test_concurrent_sync_batches_overlap(engine, oracle):
           f"{rate_all:.0f} calls/s on {nthr} ({rate_all / rate_one:.2f}x)")
 
 
+def test_concurrent_packed_batches(engine, oracle):
+    """HCRC_PACKED from several threads at once: 4 threads on their own
+    torch streams (each stream its own pre-pass scratch and verdict epochs)
+    and 4 on the synchronous entry point (the lanes' streams), alternating a
+    packed batch with a broken one (unsorted), 40 calls each -- every result
+    right, the broken ones included (their launches take the fallback)."""
+    import threading
+
+    import torch
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(14)
+    nthr, calls = 8, 40
+    jobs = []
+    for t in range(nthr):
+        offs, lens = _packed_layout(rng, 3000, 200, 2500, 5, 5, 3)
+        b = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+        bad = offs.copy()
+        bad[[10, 11]] = bad[[11, 10]]
+        jobs.append({"buf": _t(b), "good": (_t(offs), _t(lens)), "bad": (_t(bad), _t(lens)),
+                     "want_good": oracle.batch(b, offs, lens), "want_bad": oracle.batch(b, bad, lens)})
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(i):
+        try:
+            j = jobs[i]
+            st = torch.cuda.Stream() if i < nthr // 2 else None
+            for k in range(calls):
+                which = "good" if k % 2 == 0 else "bad"
+                do, dl = j[which]
+                if st is not None:
+                    out = engine.batch_device(j["buf"], do, dl, stream=st.cuda_stream, packed=True)
+                    st.synchronize()
+                else:
+                    out = torch.empty(dl.numel(), dtype=torch.int32, device="cuda")
+                    rc = lib.hcrc_batch(engine._ctx, j["buf"].data_ptr(), do.data_ptr(),
+                                                dl.data_ptr(), None, out.data_ptr(), dl.numel(),
+                                                _lib.HCRC_DEVICE_PTRS | _lib.HCRC_PACKED)
+                    assert rc == 0, rc
+                got = out.cpu().numpy().view(np.uint32)
+                if not np.array_equal(got, j["want_" + which]):
+                    errors.append((i, k, which, int((got != j["want_" + which]).sum())))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((i, repr(e)))
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(nthr)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=200)
+    assert not errors, errors[:5]
+
+
 def test_concurrent_host_batches_pageable(engine, oracle):
     """8 threads of pageable host batches (pack into pinned staging, H2D,
     kernel, D2H) at once: all results right; the aggregate rate is printed
