@@ -871,9 +871,10 @@ def test_sync_batch_balance_and_packed_flags(engine, oracle):
 def test_packed_stream_only_matches_default():
     """The packed kernel hands batches that suit run_ea (aligned 4 KiB blocks,
     table blocks, spans of >= 16 KiB) to it; with WIPDB_PS_ONLY=1 run_ps takes
-    them too.  Those shapes through run_ps, with inits and the masked output,
-    equal the default pipeline's CRCs (itself checked against the oracle
-    above), over a few hundred MiB each."""
+    them too.  Those shapes through run_ps -- and spans of 1..9 MiB, a
+    register carried over thousands of pages -- with inits and the masked
+    output, equal the default pipeline's CRCs (itself checked against the
+    oracle above), over a few hundred MiB each."""
     code = (
         "import numpy as np, torch\n"
         "from wipdb_amd import Engine\n"
@@ -883,7 +884,8 @@ def test_packed_stream_only_matches_default():
         "    return start + np.concatenate([[0], np.cumsum(l + g)[:-1]]).astype(np.uint64), l.astype(np.uint32)\n"
         "cases = {'tblocks': lay(60000, 4097, 4225, 4), 'a4k': (np.arange(60000, dtype=np.uint64) * 4096,\n"
         "         np.full(60000, 4096, np.uint32)), 'b65536': lay(4000, 65536, 73728, 5, 3),\n"
-        "         'b16k': lay(15000, 16384, 18432, 0, 1)}\n"
+        "         'b16k': lay(15000, 16384, 18432, 0, 1),\n"
+        "         'mib': lay(40, 1 << 20, 9 << 20, 3, 5)}\n"
         "bad = []\n"
         "with Engine(0) as eng:\n"
         "    size = max(int((o + l).max()) for o, l in cases.values()) + 64\n"
