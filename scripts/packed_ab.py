@@ -9,7 +9,8 @@ compared over the whole batch.
 Shapes: b512 b1024 b2048 b4096 b8192 b65536 (one Zipf bucket, SST-packed,
 gap 5, 2 GiB), mix (config 3's Zipf mix), tblocks (WriteRawBlock spans
 4097..4225 + 4-byte trailer), a4k (1 Mi aligned 4 KiB blocks, the
-headline's).  --only runs one mode (for rocprofv3 --pmc passes)."""
+headline's), walN (WAL-record-like spans of N..2N-1 bytes behind 7-byte
+headers).  --only runs one mode (for rocprofv3 --pmc passes)."""
 import json
 import os
 import sys
@@ -31,6 +32,10 @@ def shape_of(name, rng, nbytes):
     elif name == "tblocks":
         l = rng.integers(4097, 4226, nbytes // 4230).astype(np.uint32)
         o = np.concatenate([[0], np.cumsum(l.astype(np.uint64) + 4)[:-1]]).astype(np.uint64) + 3
+    elif name.startswith("wal"):  # walN: WAL-record-like spans N..2N-1 B, 7-byte headers between
+        b = int(name[3:])
+        l = rng.integers(b, 2 * b, int(nbytes // (1.5 * b + 7))).astype(np.uint32)
+        o = np.concatenate([[0], np.cumsum(l.astype(np.uint64) + 7)[:-1]]).astype(np.uint64) + 7
     elif name == "a4k":
         n = 2 * nbytes // 4096
         o, l = np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096, np.uint32)

@@ -749,6 +749,11 @@ int main(int argc, char** argv) {
       auto o3 = Packed(l, 3, 5);
       for (size_t i = 400; i < o3.size(); ++i) o3[i] += 5000;  // a gap of 5 KiB
       RunPacked("not packed: a 5 KiB gap", buf.data(), buf.size(), o3, l, nullptr, false, 3, 0, false);
+      // WAL-like records behind 7-byte headers: runs of spans under the
+      // stream minimum (sparse enough to pass the density check)
+      auto l5 = lens_of(1500, 40, 95);
+      RunPacked("not packed: runs of short spans", buf.data(), buf.size(), Packed(l5, 7, 7), l5, nullptr,
+                false, 3, 0, false);
       auto l4 = lens_of(1200, 5, 60);
       RunPacked("not packed: dense short spans", buf.data(), buf.size(), Packed(l4, 1, 7), l4, nullptr,
                 false, 3, 0, false);

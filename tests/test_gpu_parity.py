@@ -911,8 +911,9 @@ def test_packed_prepass_verdicts():
     """Which pipeline a HCRC_PACKED batch takes (test build: the pre-pass's
     words of the last packed launch).  Packed shapes -- 512 B..2 KiB, table
     blocks, aligned 4 KiB, 64 KiB spans, short / empty spans among them --
-    are streamed (meta[0] == 0); unsorted, overlapping, a 5 KiB gap and
-    dense few-byte spans fall back with the matching kPsBad* bit."""
+    are streamed (meta[0] == 0); unsorted, overlapping, a 5 KiB gap, dense
+    few-byte spans and runs of spans under the stream minimum (WAL records)
+    fall back with the matching kPsBad* bit."""
     assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
     code = (
         "import ctypes, json, numpy as np, torch\n"
@@ -937,6 +938,7 @@ def test_packed_prepass_verdicts():
         "o4 = o.copy(); o4[700:] += 5000\n"
         "cases['gap5k'] = (o4, l)\n"
         "cases['dense'] = lay(20000, 5, 60, 7)\n"
+        "cases['wal'] = lay(20000, 40, 95, 7)\n"
         "cases['again'] = cases['512-2k']\n"
         "res = {}\n"
         "with Engine(0) as eng:\n"
@@ -967,6 +969,7 @@ def test_packed_prepass_verdicts():
     for k in ("unsorted", "overlap", "gap5k"):
         assert res[k][0] & 1, (k, res[k])
     assert res["dense"][0] & 2, res["dense"]
+    assert res["wal"][0] & 4, res["wal"]  # runs of short spans (kPsBadShort)
 
 
 def _run_device_packed(engine, buf, offs, lens):

@@ -115,6 +115,10 @@ constexpr uint32_t kFaultPsDesk = 0x4;
 // span's start offset (u64).  The chunk index first[C + 1] follows them.
 constexpr uint32_t kPsMetaWords = 8;
 constexpr uint32_t kPsBad = 1u, kPsBadDense = 2u;
+// run_ps computes spans shorter than its stream minimum byte by byte from
+// memory; a run of 8 of them (WAL records) sends the batch to the
+// lane-packed pipeline instead
+constexpr uint32_t kPsBadShort = 4u;
 
 // Size classes (HCRC_SPLIT_SMALL).  A span of n bytes at address a covers
 // f = (a % 16 + n) / 16 full chunks of its 16-byte grid.  Class 4 (16-lane

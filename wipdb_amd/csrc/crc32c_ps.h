@@ -83,6 +83,7 @@ constexpr uint32_t kPsMinStream = 96;   // spans shorter than this are computed 
                                         // (a stream span's stream part is then >= 64 bytes)
 constexpr uint32_t kPsMaxGap = 4096;    // a larger gap could leave a page of no span's bytes
 constexpr uint32_t kPsDense = 62;       // spans i, i + 62 start >= 4 KiB apart
+constexpr uint32_t kPsShortRun = 8;     // this many short spans in a row: not for run_ps
 constexpr uint32_t kPsDenseBytes = 1600;  // a desk of spans shorter on average plans a page ahead
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
@@ -148,6 +149,11 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
     }
     for (uint64_t k = cp + 1u; k <= c; ++k) first[k] = static_cast<uint32_t>(i);
     if (i + kPsDense < n && off[i + kPsDense] - a < 4096u) bad |= kPsBadDense;
+    if (len[i] < kPsMinStream && i + kPsShortRun <= n) {  // a run of short spans
+      uint32_t k = 1;
+      while (k < kPsShortRun && len[i + k] < kPsMinStream) ++k;
+      if (k == kPsShortRun) bad |= kPsBadShort;
+    }
     if (i + kPsDense < n && off[i + kPsDense] < a) bad |= kPsBad;
     if (i == n - 1)
       for (uint64_t k = c + 1u; k <= C; ++k) first[k] = static_cast<uint32_t>(n);
