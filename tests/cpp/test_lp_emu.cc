@@ -324,7 +324,8 @@ void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std:
   constexpr uint32_t kEpoch = 7;
   std::vector<uint32_t> first(C + 1, 0xFFFFFFFFu), meta(kPsMetaWords, 0u);
   meta[0] = (kEpoch - 1) << 4 | kPsBad;
-  const uint32_t pgrid = static_cast<uint32_t>(std::min<size_t>((n + 255) / 256, 8));
+  static_assert(kThreads == kPsIndexThreads, "emu::launch runs kThreads lanes a workgroup");
+  const uint32_t pgrid = static_cast<uint32_t>(std::min<size_t>((n + kPsIndexThreads - 1) / kPsIndexThreads, 8));
   emu::launch(pgrid ? pgrid : 1, [&] {
     crc32c_ps_index_kernel(offs.data(), lens.data(), n, C, first.data(), meta.data(), kEpoch);
   });

@@ -119,6 +119,10 @@ constexpr uint32_t kPsBad = 1u, kPsBadDense = 2u;
 // memory; a run of 8 of them (WAL records) sends the batch to the
 // lane-packed pipeline instead
 constexpr uint32_t kPsBadShort = 4u;
+// the pre-pass kernel's workgroup (16 waves: one verdict atomic per 1024
+// threads) and its LDS (a word per wave)
+constexpr uint32_t kPsIndexThreads = 1024;
+constexpr uint32_t kPsIndexLds = kPsIndexThreads / 64u * 4u;
 
 // Size classes (HCRC_SPLIT_SMALL).  A span of n bytes at address a covers
 // f = (a % 16 + n) / 16 full chunks of its 16-byte grid.  Class 4 (16-lane

@@ -1097,14 +1097,12 @@ template __global__ void crc32c_lds_packed_kernel<1>(const uint8_t*, const uint6
 
 // The packed batch's pre-pass (crc32c_ps.h ps_index); epoch: the launch's
 // tag of the verdict word (1 .. 2^28 - 1, the host's per-stream count).
-__global__ __launch_bounds__(256) void crc32c_ps_index_kernel(const uint64_t* __restrict__ offsets,
-                                                              const uint32_t* __restrict__ lengths,
-                                                              uint64_t count, uint32_t C,
-                                                              uint32_t* __restrict__ first,
-                                                              uint32_t* __restrict__ meta,
-                                                              uint32_t epoch) {
-  const uint64_t nt = static_cast<uint64_t>(group_count()) * 256u;
-  const uint64_t tid = static_cast<uint64_t>(group_id()) * 256u + (lane_tid() & 255u);
+// kPsIndexThreads threads a workgroup, kPsIndexLds bytes of LDS.
+__global__ __launch_bounds__(kPsIndexThreads) void crc32c_ps_index_kernel(
+    const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths, uint64_t count,
+    uint32_t C, uint32_t* __restrict__ first, uint32_t* __restrict__ meta, uint32_t epoch) {
+  const uint64_t nt = static_cast<uint64_t>(group_count()) * kPsIndexThreads;
+  const uint64_t tid = static_cast<uint64_t>(group_id()) * kPsIndexThreads + lane_tid();
   ps_index(nullptr, offsets, lengths, count, C, first, meta, tid, nt, epoch);
 }
 

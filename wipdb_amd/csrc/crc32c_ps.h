@@ -53,7 +53,8 @@
 // metaindex block).
 //
 // Work: the pre-pass (ps_index_kernel) checks the batch (sorted, no overlap,
-// gaps < 4 KiB, at most 62 spans starting in any 4 KiB) and cuts the
+// gaps < 4 KiB, at most 62 spans starting in any 4 KiB, no run of 8 spans
+// under 96 bytes -- WAL records, which run_lp does faster) and cuts the
 // covering range into C equal byte chunks, first[c] = the first span starting
 // in chunk c: one chunk per wave (C = 16 per workgroup); a chunk is its
 // spans, whole.  The SIMDs issue oldest-first, which on equal shares makes a
@@ -105,11 +106,12 @@ __device__ __forceinline__ uint32_t low_bytes(uint32_t b) {
 
 // ---------------------------------------------------------------------------
 // The pre-pass: check the batch, cut its covering range into C chunks.
-// Thread i handles span i (grid-stride); first[] written where the chunk
-// index steps (first has C + 1 entries, first[C] = n).  The verdict word
-// meta[0] is tagged with the launch's epoch (its stream's count of packed
-// launches): thread 0 raises it to epoch << 4, a thread that finds the
-// batch broken to epoch << 4 | kPsBad*, so it needs no clearing between
+// Thread i handles span i (grid-stride, a wave's 64 spans consecutive);
+// first[] written where the chunk index steps (first has C + 1 entries,
+// first[C] = n).  The verdict word meta[0] is tagged with the launch's
+// epoch (its stream's count of packed launches): thread 0 raises it to
+// epoch << 4, a workgroup that finds the batch broken to epoch << 4 |
+// kPsBad* (and its waves stop there), so it needs no clearing between
 // launches (a stale word is an older epoch, lower).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* off,
@@ -129,37 +131,65 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
     meta[3] = static_cast<uint32_t>(lo);
     meta[4] = static_cast<uint32_t>(lo >> 32);
   }
+  // a wave takes 64 consecutive spans a step (wave-uniform trip count: the
+  // ballots below see every lane)
   uint32_t bad = 0;
-  for (uint64_t i = tid; i < n; i += nthreads) {
-    const uint64_t a = off[i];
-    uint64_t c = a >= lo ? (a - lo) / cb : 0u;
-    if (a < lo || c >= C) {
-      bad |= kPsBad;
-      c = C - 1u;
+  for (uint64_t w0 = tid & ~uint64_t(63); w0 < n; w0 += nthreads) {
+    const uint64_t i = w0 + (tid & 63u);
+    bool shrt = false;
+    if (i < n) {
+      const uint64_t a = off[i];
+      uint64_t c = a >= lo ? (a - lo) / cb : 0u;
+      if (a < lo || c >= C) {
+        bad |= kPsBad;
+        c = C - 1u;
+      }
+      uint64_t cp = 0;  // chunks (cp, c] start at span i
+      if (i == 0) {
+        cp = 0;
+        first[0] = 0;
+      } else {
+        const uint64_t ap = off[i - 1], bp = ap + len[i - 1];
+        if (a < bp || a - bp >= kPsMaxGap) bad |= kPsBad;
+        cp = ap >= lo ? (ap - lo) / cb : 0u;
+        if (cp > c) cp = c;
+      }
+      for (uint64_t k = cp + 1u; k <= c; ++k) first[k] = static_cast<uint32_t>(i);
+      if (i + kPsDense < n && off[i + kPsDense] - a < 4096u) bad |= kPsBadDense;
+      if (i + kPsDense < n && off[i + kPsDense] < a) bad |= kPsBad;
+      if (i == n - 1)
+        for (uint64_t k = c + 1u; k <= C; ++k) first[k] = static_cast<uint32_t>(n);
+      shrt = len[i] < kPsMinStream;
     }
-    uint64_t cp = 0;  // chunks (cp, c] start at span i
-    if (i == 0) {
-      cp = 0;
-      first[0] = 0;
-    } else {
-      const uint64_t ap = off[i - 1], bp = ap + len[i - 1];
-      if (a < bp || a - bp >= kPsMaxGap) bad |= kPsBad;
-      cp = ap >= lo ? (ap - lo) / cb : 0u;
-      if (cp > c) cp = c;
-    }
-    for (uint64_t k = cp + 1u; k <= c; ++k) first[k] = static_cast<uint32_t>(i);
-    if (i + kPsDense < n && off[i + kPsDense] - a < 4096u) bad |= kPsBadDense;
-    if (len[i] < kPsMinStream && i + kPsShortRun <= n) {  // a run of short spans
-      uint32_t k = 1;
-      while (k < kPsShortRun && len[i + k] < kPsMinStream) ++k;
-      if (k == kPsShortRun) bad |= kPsBadShort;
-    }
-    if (i + kPsDense < n && off[i + kPsDense] < a) bad |= kPsBad;
-    if (i == n - 1)
-      for (uint64_t k = c + 1u; k <= C; ++k) first[k] = static_cast<uint32_t>(n);
+    // a run of kPsShortRun short spans among the step's 64 (bit j of m: spans
+    // j..j+7 all short; a run across two steps may go unseen -- the verdict
+    // is a speed choice, every pipeline computes short spans exactly).  One
+    // ballot, no loads: a per-span look-ahead loop cost 150 us on 20 Mi
+    // spans (profiles/r05ar_wal_kernels.txt).
+    static_assert(kPsShortRun == 8, "the run test below is three shift-ANDs");
+    uint64_t m = ballot(shrt);
+    m &= m >> 1;
+    m &= m >> 2;
+    m &= m >> 4;
+    if (m) bad |= kPsBadShort;
+    if (ballot(bad != 0u)) break;  // (broken: first[] goes unread, the verdict is raised below)
   }
   (void)base;
-  if (tid == 0 || bad) global_max(meta, (epoch << 4) | bad);
+  // one atomic per workgroup: a broken batch of tiny spans has every thread
+  // of the grid find it so, and same-word device atomics serialize (~11 ns
+  // each: 512 Ki of them took 6 ms, 8 Ki 98 us -- profiles/r05ao_wal_ab.log,
+  // r05ar_wal_kernels.txt).  The waves' ORs (ballot per bit) meet in LDS words
+  // 0..15 (the kernel's 64 bytes), thread 0 raises the verdict.
+  uint32_t w = 0;
+  for (uint32_t b = 1u; b <= (kPsBad | kPsBadDense | kPsBadShort); b <<= 1)
+    if (ballot((bad & b) != 0u)) w |= b;
+  const uint32_t t = lane_tid();
+  if ((t & 63u) == 0u) lds_st_sync((t >> 6) * 4u, w);
+  wg_sync();
+  if (t == 0) {
+    for (uint32_t k = 1; k < kPsIndexThreads / 64u; ++k) w |= lds_ld_sync(k * 4u);
+    if (w != 0u || tid == 0) global_max(meta, (epoch << 4) | w);
+  }
 }
 
 // A page's events to the lanes of their stripes: the lanes with `ev`

@@ -660,9 +660,11 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         }
         uint32_t* meta = ps->d;
         uint32_t* first = meta + lk::kPsMetaWords;
-        const int pgrid = static_cast<int>(
-            std::max<size_t>(1, std::min<size_t>((n + 255) / 256, size_t(ctx->num_cu) * 8)));
-        hipLaunchKernelGGL(lk::crc32c_ps_index_kernel, dim3(pgrid), dim3(256), 0, st, off + pos,
+        const int pgrid = static_cast<int>(std::max<size_t>(
+            1, std::min<size_t>((n + lk::kPsIndexThreads - 1) / lk::kPsIndexThreads,
+                                size_t(ctx->num_cu) * 2)));
+        hipLaunchKernelGGL(lk::crc32c_ps_index_kernel, dim3(pgrid), dim3(lk::kPsIndexThreads),
+                           lk::kPsIndexLds, st, off + pos,
                            len + pos, static_cast<uint64_t>(n), C, first, meta, ps->epoch);
 #ifdef WIPDB_HCRC_TEST_HOOKS
         // (test build: the pre-pass's verdict and chunk size, for the tests
