@@ -123,6 +123,8 @@ constexpr uint32_t kPsBadShort = 4u;
 // threads) and its LDS (a word per wave)
 constexpr uint32_t kPsIndexThreads = 1024;
 constexpr uint32_t kPsIndexLds = kPsIndexThreads / 64u * 4u;
+// steps of 64 spans a wave loads at once (memory-level parallelism)
+constexpr uint32_t kPsIndexSteps = 4;
 
 // Size classes (HCRC_SPLIT_SMALL).  A span of n bytes at address a covers
 // f = (a % 16 + n) / 16 full chunks of its 16-byte grid.  Class 4 (16-lane

@@ -131,47 +131,81 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
     meta[3] = static_cast<uint32_t>(lo);
     meta[4] = static_cast<uint32_t>(lo >> 32);
   }
-  // a wave takes 64 consecutive spans a step (wave-uniform trip count: the
-  // ballots below see every lane)
-  uint32_t bad = 0;
-  for (uint64_t w0 = tid & ~uint64_t(63); w0 < n; w0 += nthreads) {
-    const uint64_t i = w0 + (tid & 63u);
-    bool shrt = false;
-    if (i < n) {
-      const uint64_t a = off[i];
-      uint64_t c = a >= lo ? (a - lo) / cb : 0u;
-      if (a < lo || c >= C) {
-        bad |= kPsBad;
-        c = C - 1u;
+  // the chunk of address a: (a - lo) / cb in 32 bits (cb is whole pages;
+  // the page index of any address of a device buffer fits, one that does
+  // not is past the range: C, broken).  (Cheaper than the 64-bit division;
+  // the pass's time did not move, profiles/r05ar_wal_kernels.txt r05as.)
+  const uint32_t cbp = static_cast<uint32_t>(cb >> 12);
+  auto chunk_of = [lo, cbp, C](uint64_t a) -> uint64_t {
+    if (a < lo) return 0u;
+    const uint64_t v = (a - lo) >> 12;
+    return (v >> 32) ? uint64_t(C) : uint64_t(static_cast<uint32_t>(v) / cbp);
+  };
+  // a wave takes 64 consecutive spans a step, kPsIndexSteps steps an
+  // iteration with all their loads issued first (the pass is latency-bound:
+  // 21 -> 16 us on 3.5 Mi spans, 71 -> 42 us on 21 Mi); the trip count
+  // is wave-uniform, so the ballots below see every lane.  Chunks of 16 TiB
+  // and more (no device holds such a batch) would not divide in 32 bits:
+  // broken.
+  constexpr uint32_t U = kPsIndexSteps;
+  uint32_t bad = (cb >> 44) ? kPsBad : 0u;
+  for (uint64_t w0 = tid & ~uint64_t(63); w0 < n; w0 += U * nthreads) {
+    uint64_t A[U], AP[U], AD[U];
+    uint32_t LP[U], L[U];
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+      const uint64_t i = w0 + j * nthreads + (tid & 63u);
+      A[j] = AP[j] = AD[j] = 0;
+      LP[j] = L[j] = 0;
+      if (i < n) {
+        A[j] = off[i];
+        L[j] = len[i];
+        if (i > 0) {
+          AP[j] = off[i - 1];
+          LP[j] = len[i - 1];
+        }
+        if (i + kPsDense < n) AD[j] = off[i + kPsDense];
       }
-      uint64_t cp = 0;  // chunks (cp, c] start at span i
-      if (i == 0) {
-        cp = 0;
-        first[0] = 0;
-      } else {
-        const uint64_t ap = off[i - 1], bp = ap + len[i - 1];
-        if (a < bp || a - bp >= kPsMaxGap) bad |= kPsBad;
-        cp = ap >= lo ? (ap - lo) / cb : 0u;
-        if (cp > c) cp = c;
-      }
-      for (uint64_t k = cp + 1u; k <= c; ++k) first[k] = static_cast<uint32_t>(i);
-      if (i + kPsDense < n && off[i + kPsDense] - a < 4096u) bad |= kPsBadDense;
-      if (i + kPsDense < n && off[i + kPsDense] < a) bad |= kPsBad;
-      if (i == n - 1)
-        for (uint64_t k = c + 1u; k <= C; ++k) first[k] = static_cast<uint32_t>(n);
-      shrt = len[i] < kPsMinStream;
     }
-    // a run of kPsShortRun short spans among the step's 64 (bit j of m: spans
-    // j..j+7 all short; a run across two steps may go unseen -- the verdict
-    // is a speed choice, every pipeline computes short spans exactly).  One
-    // ballot, no loads: a per-span look-ahead loop cost 150 us on 20 Mi
-    // spans (profiles/r05ar_wal_kernels.txt).
-    static_assert(kPsShortRun == 8, "the run test below is three shift-ANDs");
-    uint64_t m = ballot(shrt);
-    m &= m >> 1;
-    m &= m >> 2;
-    m &= m >> 4;
-    if (m) bad |= kPsBadShort;
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+      const uint64_t i = w0 + j * nthreads + (tid & 63u);
+      bool shrt = false;
+      if (i < n) {
+        const uint64_t a = A[j];
+        uint64_t c = chunk_of(a);
+        if (a < lo || c >= C) {
+          bad |= kPsBad;
+          c = C - 1u;
+        }
+        uint64_t cp = 0;  // chunks (cp, c] start at span i
+        if (i == 0) {
+          first[0] = 0;
+        } else {
+          const uint64_t ap = AP[j], bp = ap + LP[j];
+          if (a < bp || a - bp >= kPsMaxGap) bad |= kPsBad;
+          cp = chunk_of(ap);
+          if (cp > c) cp = c;
+        }
+        for (uint64_t k = cp + 1u; k <= c; ++k) first[k] = static_cast<uint32_t>(i);
+        if (i + kPsDense < n && AD[j] - a < 4096u) bad |= kPsBadDense;
+        if (i + kPsDense < n && AD[j] < a) bad |= kPsBad;
+        if (i == n - 1)
+          for (uint64_t k = c + 1u; k <= C; ++k) first[k] = static_cast<uint32_t>(n);
+        shrt = L[j] < kPsMinStream;
+      }
+      // a run of kPsShortRun short spans among the step's 64 (bit b of m:
+      // spans b..b+7 all short; a run across two steps may go unseen -- the
+      // verdict is a speed choice, every pipeline computes short spans
+      // exactly).  One ballot, no loads: a per-span look-ahead loop cost
+      // 150 us on 20 Mi spans (profiles/r05ar_wal_kernels.txt).
+      static_assert(kPsShortRun == 8, "the run test below is three shift-ANDs");
+      uint64_t m = ballot(shrt);
+      m &= m >> 1;
+      m &= m >> 2;
+      m &= m >> 4;
+      if (m) bad |= kPsBadShort;
+    }
     if (ballot(bad != 0u)) break;  // (broken: first[] goes unread, the verdict is raised below)
   }
   (void)base;
