@@ -201,6 +201,9 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
       // 150 us on 20 Mi spans (profiles/r05ar_wal_kernels.txt).
       static_assert(kPsShortRun == 8, "the run test below is three shift-ANDs");
       uint64_t m = ballot(shrt);
+      // (or half the step's spans short: WAL records of 64..127 B rarely
+      // make a run of 8, and the look stops at the first step)
+      if (__builtin_popcountll(m) >= 32) bad |= kPsBadShort;
       m &= m >> 1;
       m &= m >> 2;
       m &= m >> 4;
