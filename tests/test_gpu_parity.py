@@ -939,6 +939,7 @@ def test_packed_prepass_verdicts():
         "cases['gap5k'] = (o4, l)\n"
         "cases['dense'] = lay(20000, 5, 60, 7)\n"
         "cases['wal'] = lay(20000, 40, 95, 7)\n"
+        "cases['wal64'] = lay(20000, 64, 127, 7)\n"
         "cases['again'] = cases['512-2k']\n"
         "res = {}\n"
         "with Engine(0) as eng:\n"
@@ -970,6 +971,7 @@ def test_packed_prepass_verdicts():
         assert res[k][0] & 1, (k, res[k])
     assert res["dense"][0] & 2, res["dense"]
     assert res["wal"][0] & 4, res["wal"]  # runs of short spans (kPsBadShort)
+    assert res["wal64"][0] & 4, res["wal64"]  # half of them short
 
 
 def _run_device_packed(engine, buf, offs, lens):

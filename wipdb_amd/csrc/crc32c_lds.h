@@ -116,8 +116,8 @@ constexpr uint32_t kFaultPsDesk = 0x4;
 constexpr uint32_t kPsMetaWords = 8;
 constexpr uint32_t kPsBad = 1u, kPsBadDense = 2u;
 // run_ps computes spans shorter than its stream minimum byte by byte from
-// memory; a run of 8 of them (WAL records) sends the batch to the
-// lane-packed pipeline instead
+// memory; a run of 8 of them, or 32 among a step's 64 spans (WAL records),
+// sends the batch to the lane-packed pipeline instead
 constexpr uint32_t kPsBadShort = 4u;
 // the pre-pass kernel's workgroup (16 waves: one verdict atomic per 1024
 // threads) and its LDS (a word per wave)

@@ -54,9 +54,9 @@
 //
 // Work: the pre-pass (ps_index_kernel) checks the batch (sorted, no overlap,
 // gaps < 4 KiB, at most 62 spans starting in any 4 KiB, no run of 8 spans
-// under 96 bytes -- WAL records, which run_lp does faster) and cuts the
-// covering range into C equal byte chunks, first[c] = the first span starting
-// in chunk c: one chunk per wave (C = 16 per workgroup); a chunk is its
+// under 96 bytes nor 32 among 64 -- WAL records, which run_lp does faster)
+// and cuts the covering range into C equal byte chunks, first[c] = the first
+// span starting in chunk c: one chunk per wave (C = 16 per workgroup); a chunk is its
 // spans, whole.  The SIMDs issue oldest-first, which on equal shares makes a
 // wave's speed its age (the last wave of a SIMD up to 15 % behind the first):
 // every 4 pages a wave compares its pages with its workgroup's and takes a
