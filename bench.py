@@ -24,7 +24,11 @@ The compare kernels torch uses for the check are loaded before the window
 (their first use cost ~250 ms of GPU idle inside it), so the
 window is continuous GPU work; the line reports the mean kernel time of the
 window's first and last 10 launches, so the settling is visible
-("precondition").
+("precondition").  The W warmup steps are queued right behind the window
+and its per-launch times are read only after the timed region: a host pause
+of >= 2 ms between the window and the timed steps (round 5 read 382 event
+pairs there) let the memory clocks drop and cost the timed launches 4-6 %
+(profiles/r06a_gap_*.log, scripts/gap_probe.py).
 
 Also printed in the same JSON line:
   roofline      the CRC kernel's average launch time from HIP events on the
@@ -44,10 +48,16 @@ Also printed in the same JSON line:
                 DRAM), and on every CPU this process may use; rank 0, N=1.
   parity        the reference CRCs vs the GPU's for every block of the shard
                 (N = 1) or a 64 Ki-block sample per rank (N > 1).
-  readstream_ceiling
-                this box's plain read-stream kernel over the same shard (the
-                same-box HBM ceiling), after the timed region; roofline
-                frac_of_readstream = achieved / its read rate.
+  ceiling       this box's ceiling for the kernel: the spans kernel's own
+                memory side alone (hcrc_dma_ceiling_async -- the table image,
+                the unit deal, the same LDS-DMAs and slot reads, 4 B stored
+                per block, no CRC) over the same shard, after the timed
+                region; roofline frac_of_ceiling = ceiling time / kernel
+                time; also the two alternating back to back
+                (frac_of_ceiling_alternating).  roofline.timed_dispatch_first
+                = the index of the first timed launch among this process's
+                spans-kernel dispatches (scripts/trace_timed.py picks the K
+                timed ones out of a rocprofv3 kernel trace).
   config3_mixed, table_blocks, verified_table_blocks, config5_pcie
                 (rank 0, N = 1, after the headline; --no-extra skips them)
                 BASELINE configs[2] and [4] under the same clock: config 3's
@@ -92,11 +102,12 @@ def parse():
                    help="HIP events around every timed launch (per-launch kernel times) or "
                         "only around the timed region (no event between launches)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--poll-events", action="store_true",
+                   help="diagnostic: poll the timed region's events before the synchronize")
     p.add_argument("--cpu-seconds", type=float, default=5.0,
                    help="minimum time of the 1-thread reference baseline (whole passes)")
-    p.add_argument("--no-readstream", action="store_true",
-                   help="skip the read-stream ceiling kernel (timed after the headline)")
-    p.add_argument("--readstream", action="store_true", help=argparse.SUPPRESS)  # (the default)
+    p.add_argument("--no-ceiling", "--no-readstream", dest="no_ceiling", action="store_true",
+                   help="skip the same-box ceiling kernel (timed after the headline)")
     p.add_argument("--no-extra", action="store_true",
                    help="skip configs 3 / 5 and the table-block shapes after the headline")
     return p.parse_args()
@@ -242,8 +253,15 @@ def main():
             eng.batch_strided_device(data, BLOCK, BLOCK, nblk, 0, dst, stream=stream.cuda_stream)
 
     # precondition: untimed back-to-back launches of the step (at least
-    # precondition_ms of GPU time), every output compared with the first
+    # precondition_ms of GPU time), every output compared with the first.
+    # The warmup steps follow on the stream with no host wait in between, and
+    # the per-launch times are read only after the timed region: a host-side
+    # pause of even 2 ms lets the memory clocks drop, and the next ~20
+    # launches then run 5-18 % slower (profiles/r06a_gap_*.log,
+    # scripts/gap_probe.py) -- the timed steps must start from the settled
+    # state the precondition reached, not from an idle card.
     pre = {"launches": 0, "gpu_ms": 0.0, "identical_outputs": True}
+    pev = []
     if a.precondition_ms > 0:
         ref = torch.empty_like(out)
         scratch = torch.empty_like(out)
@@ -265,16 +283,7 @@ def main():
             pe.record(stream)
             mism += (scratch != ref).sum()
         e1.record(stream)
-        torch.cuda.synchronize(dev)
-        pk = [ps.elapsed_time(pe) for ps, pe in pev]
-        pre = {"launches": n + 2, "gpu_ms": round(e0.elapsed_time(e1), 2),
-               "kernel_ms_sum": round(sum(pk), 2),
-               "first10_kernel_ms": round(sum(pk[:10]) / 10, 4),
-               "last10_kernel_ms": round(sum(pk[-10:]) / 10, 4),
-               "identical_outputs": int(mism.item()) == 0,
-               "why": "after idle, back-to-back launches run up to 1.5x slower for ~30-60 ms while "
-                      "the SMU settles the power-capped clocks (profiles/r02_launch_series.json)"}
-        del ref, scratch
+        pre["launches"] = n + 2
 
     for _ in range(a.warmup):
         step()
@@ -293,36 +302,94 @@ def main():
             e.record(stream)
     else:
         ev[0][0].record(stream)
-        for _ in range(a.steps):
+        for i in range(a.steps):
             step()
+            if i == 0:
+                t_first = time.perf_counter()
         ev[0][1].record(stream)
+    t_queued = time.perf_counter()
+    t_started = None
+    if a.poll_events and a.events != "step":  # (diagnostic: when did the GPU reach the bracket?)
+        while not ev[0][0].query():
+            pass
+        t_started = time.perf_counter()
+        while not ev[0][1].query():
+            pass
     torch.cuda.synchronize(dev)
+    t_synced = time.perf_counter()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    host_ms = {"first_launch_returned": round((t_first - t0) * 1e3, 3) if a.events != "step" else None,
+               "all_queued": round((t_queued - t0) * 1e3, 3),
+               "gpu_started_seen": None if t_started is None else round((t_started - t0) * 1e3, 3),
+               "synced": round((t_synced - t0) * 1e3, 3), "elapsed": round(elapsed * 1e3, 3)}
     kern_ms = [s.elapsed_time(e) * nev / a.steps for s, e in ev]
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
     elapsed_max = max_over_ranks(elapsed, dev)
     kern_avg_ms = max_over_ranks(kern_avg_ms, dev)
 
-    rs = None
-    if not a.no_readstream:
-        rs_out = torch.empty(nblk, dtype=torch.int32, device=dev)
-        for _ in range(2):
-            eng.readstream_device(data, BLOCK, BLOCK, nblk, rs_out, stream=stream.cuda_stream)
+    if pev:
+        pk = [ps.elapsed_time(pe) for ps, pe in pev]
+        pre.update({"gpu_ms": round(e0.elapsed_time(e1), 2),
+                    "kernel_ms_sum": round(sum(pk), 2),
+                    "first10_kernel_ms": round(sum(pk[:10]) / 10, 4),
+                    "last10_kernel_ms": round(sum(pk[-10:]) / 10, 4),
+                    "identical_outputs": int(mism.item()) == 0,
+                    "why": "after idle, back-to-back launches run up to 1.5x slower for ~30-60 ms "
+                           "while the SMU raises the clocks again (profiles/r02_launch_series.json, "
+                           "r06a_gap_*.log); the warmup and timed steps follow with no host pause"})
+        del ref, scratch, pev
+
+    ceil = None
+    if not a.no_ceiling and a.mode == "spans":
+        # The same-box ceiling: the spans kernel's memory side alone on the
+        # same shard (hcrc_dma_ceiling_async: the image load, the unit deal,
+        # the same LDS-DMAs and slot reads, 4 B stored per block, no CRC).
+        # Warmed back to back for >= 100 ms from the timed region's end, then
+        # K ceiling launches and K more CRC launches alternating in rounds of
+        # K / 2, one event pair per run, nothing between them on the stream.
+        c_out = torch.empty(nblk, dtype=torch.int32, device=dev)
         s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s0.record(stream)
-        for _ in range(a.steps):
-            eng.readstream_device(data, BLOCK, BLOCK, nblk, rs_out, stream=stream.cuda_stream)
+        eng.dma_ceiling_device(data, BLOCK, nblk, c_out, stream=stream.cuda_stream)
         s1.record(stream)
         torch.cuda.synchronize(dev)
-        rs_ms = s0.elapsed_time(s1) / a.steps
-        rs = {"kernel": "readstream_kernel", "avg_ms": round(rs_ms, 4),
-              "read_GBps": round(nblk * BLOCK / rs_ms / 1e6, 1),
-              "what": "this box's plain read stream over the same shard, after the timed region"}
-        del rs_out
+        nw = max(16, int(100.0 / max(s0.elapsed_time(s1), 1e-3)))
+        for _ in range(nw):
+            eng.dma_ceiling_device(data, BLOCK, nblk, c_out, stream=stream.cuda_stream)
+        half = max(1, a.steps // 2)
+        runs = []
+        for r in range(4):
+            b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            b0.record(stream)
+            for _ in range(half):
+                if r % 2 == 0:
+                    eng.dma_ceiling_device(data, BLOCK, nblk, c_out, stream=stream.cuda_stream)
+                else:
+                    step()
+            b1.record(stream)
+            runs.append((r % 2, b0, b1))
+        torch.cuda.synchronize(dev)
+        cms = [b0.elapsed_time(b1) / half for k, b0, b1 in runs if k == 0]
+        kms = [b0.elapsed_time(b1) / half for k, b0, b1 in runs if k == 1]
+        c_ms, k_ms = sum(cms) / len(cms), sum(kms) / len(kms)
+        heads = data.view(nblk, BLOCK)[:, :64].contiguous().view(torch.int32)
+        want = heads[:, 0]
+        for j in range(1, 16):
+            want = torch.bitwise_xor(want, heads[:, j])
+        ceil = {"kernel": "crc32c_dma_ceiling_kernel", "avg_ms": round(c_ms, 4),
+                "GBps": round(nblk * ALGO_BYTES_PER_BLOCK / c_ms / 1e6, 1),
+                "crc_kernel_ms_alternating": round(k_ms, 4),
+                "frac_of_ceiling_alternating": round(c_ms / k_ms, 4),
+                "words_checked": int(nblk), "word_mismatches": int((c_out != want).sum().item()),
+                "what": "the spans kernel's memory side alone (table image, unit deal, the same "
+                        "LDS-DMAs and slot reads, 4 B stored per block, no CRC) over the same "
+                        "shard on this box, after the timed region; alternating with the CRC "
+                        "kernel in runs of K/2 back to back"}
+        del c_out, heads, want
 
     # parity (and, rank 0 at N = 1, the CPU baseline) on the host
     gpu_crc = out.cpu().numpy().view(np.uint32)
@@ -381,12 +448,14 @@ def main():
                 "kernel_timing": ("HIP events around each timed launch" if a.events == "step" else
                                   "HIP events around the timed launches / K"),
                 "algorithmic_bytes_per_launch": nblk * ALGO_BYTES_PER_BLOCK,
+                "timed_dispatch_first": pre["launches"] + a.warmup,
             },
+            "timed_region_host_ms": host_ms,
             "precondition": pre,
         }
-        if rs:
-            line["readstream_ceiling"] = rs
-            line["roofline"]["frac_of_readstream"] = round(achieved / rs["read_GBps"], 4)
+        if ceil:
+            line["ceiling"] = ceil
+            line["roofline"]["frac_of_ceiling"] = round(ceil["avg_ms"] / kern_avg_ms, 4)
         if cb:
             line["cpu_baseline"] = cb
         line["parity"] = par

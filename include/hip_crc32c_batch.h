@@ -261,6 +261,17 @@ int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
                           uint32_t length, uint32_t* d_out, size_t count,
                           void* stream);
 
+/* Diagnostic: the kernel's own memory ceiling.  The memory side of the
+ * spans kernel's pipeline for aligned 4 KiB blocks alone -- the table image
+ * into LDS, the same unit deal, the same four 1 KiB LDS-DMA loads per block
+ * into the wave's slot, the same slot reads, 4 bytes stored per block -- with
+ * no CRC work (out[i] = XOR of the first 64 bytes of block i).  length must be
+ * 4096, stride >= 4096.  The bench line's roofline reports the CRC kernel
+ * against this same-box ceiling (frac_of_ceiling). */
+int hcrc_dma_ceiling_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride,
+                           uint32_t length, uint32_t* d_out, size_t count,
+                           void* stream);
+
 /* Test/bench data: fills nbytes (multiple of 8, 8-byte aligned) of device
  * memory with the seeded splitmix64 stream whose 64-bit word k is
  * mix(seed + (first_word + k + 1) * 0x9E3779B97F4A7C15), so the host can

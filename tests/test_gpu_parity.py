@@ -1179,6 +1179,22 @@ def test_readstream_xor(engine):
     np.testing.assert_array_equal(got, np.bitwise_xor.reduce(words, axis=1))
 
 
+def test_dma_ceiling_reads_every_block(engine):
+    """The roofline's same-box ceiling (hcrc_dma_ceiling_async) reads every
+    block it is given: word i = XOR of block i's first 64 bytes, at a stride
+    and for a count that is not a whole round of the grid."""
+    rng = np.random.default_rng(3)
+    n, stride = 5000, 4096 + 512
+    buf = rng.integers(0, 256, (n - 1) * stride + 4096, dtype=np.uint8)
+    got = _u32(engine.dma_ceiling_device(_t(buf), stride, n))
+    heads = np.lib.stride_tricks.as_strided(buf, (n, 64), (stride, 1)).copy()
+    want = np.bitwise_xor.reduce(heads.view(np.uint32), axis=1)
+    np.testing.assert_array_equal(got, want)
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    assert lib.hcrc_dma_ceiling_async(engine._ctx, 1, 4096, 4097, 1, 1, None) == _lib.HCRC_ERR_INVALID
+
+
 def test_async_requires_device_flag(engine):
     from wipdb_amd import _lib
     lib = _lib.load()

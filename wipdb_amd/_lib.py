@@ -69,6 +69,7 @@ _PROTOS = {
     "hcrc_host_register": (_c.c_int, [_vp, _sz]),
     "hcrc_host_unregister": (_c.c_int, [_vp]),
     "hcrc_readstream_async": (_c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint32, _vp, _sz, _vp]),
+    "hcrc_dma_ceiling_async": (_c.c_int, [_vp, _vp, _c.c_uint64, _c.c_uint32, _vp, _sz, _vp]),
     "hcrc_check_spans_async": (
         _c.c_int, [_vp, _c.c_uint64, _vp, _vp, _c.c_uint32, _sz, _vp, _vp]),
     "hcrc_check_spans": (

@@ -291,6 +291,23 @@ class Engine:
               "hcrc_readstream_async")
         return out_t
 
+    def dma_ceiling_device(self, base_t, stride: int, count: int, out_t=None, stream=None):
+        """The spans kernel's memory side alone on `count` aligned 4 KiB blocks
+        at `stride` (hcrc_dma_ceiling_async): the same-box ceiling of the
+        roofline.  out[i] = XOR of the first 64 bytes of block i."""
+        import torch
+        nbytes = int(base_t.numel()) * base_t.element_size()
+        if count and (count - 1) * stride + 4096 > nbytes:
+            raise ValueError("dma_ceiling_device: the blocks run past the buffer")
+        if out_t is None:
+            out_t = torch.empty(count, dtype=torch.int32, device=base_t.device)
+        if int(out_t.numel()) < count:
+            raise ValueError("dma_ceiling_device: out is shorter than count")
+        check(self._lib.hcrc_dma_ceiling_async(self._ctx, _ptr(base_t), stride, 4096,
+                                               _ptr(out_t), count, self._stream_of(stream)),
+              "hcrc_dma_ceiling_async")
+        return out_t
+
     def fill_splitmix64_device(self, dst_t, seed: int, first_word: int = 0, stream=None):
         """Fill a device tensor with the seeded splitmix64 stream."""
         nbytes = int(dst_t.numel()) * dst_t.element_size()

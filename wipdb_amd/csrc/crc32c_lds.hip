@@ -1128,6 +1128,56 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_verify_kernel(
   else run_lp<1>(src, status, 0u, image, fault);
 }
 
+#if !defined(WIPDB_LK_EMU)
+// The memory side of run_ea alone -- the roofline's same-box ceiling
+// (hcrc_dma_ceiling_async).  Everything run_ea does with
+// memory on fixed-size 4 KiB blocks, nothing else: the 96 KiB table image
+// into LDS, the same unit deal (wg_units / grab_unit), the same four
+// 1 KiB global_load_lds_dwordx4 per block into the wave's slot (pp.cm's
+// rotated chunk order), the next block's DMA issued right after the slot is
+// read, the same slot reads, and 4 bytes stored per block. No CRC: the word
+// stored for block b is the XOR of its first 64 bytes (lane 0's stripe).
+// length must be 4096 (the host checks).
+__global__ __launch_bounds__(kThreads) void crc32c_dma_ceiling_kernel(
+    const uint8_t* __restrict__ base, uint64_t stride, uint32_t* __restrict__ out, uint64_t count,
+    const uint8_t* __restrict__ image) {
+  const uint32_t l = lane_tid() & 63u;
+  const uint32_t w = uni(lane_tid() >> 6);
+  const WgUnits units = wg_units(count, nullptr);
+  if (units.count == 0u) return;
+  load_image(image, w, l);
+  Pipe pp;
+  pp.init(l, w);
+  const uint64_t sbase = reinterpret_cast<uint64_t>(base);
+  const uint32_t o = 16u * pp.cm;
+  uint64_t s = grab_unit(l, units);
+  if (s >= count) return;
+  dma4(sbase + s * stride, pp.slot, o, o + 1024u, o + 2048u, o + 3072u);
+  uint64_t nx = grab_unit(l, units);
+  g_u32* const out32 = (g_u32*)(reinterpret_cast<uintptr_t>(out));
+  bool stored_prev = false;
+  for (;;) {
+    if (stored_prev) wait_vm<1>();
+    else wait_vm<0>();
+    uint32_t W[16];
+    pp.read(W);
+    pp.release();
+    const uint64_t cur = s;
+    s = nx;
+    if (s < count) {
+      dma4(sbase + s * stride, pp.slot, o, o + 1024u, o + 2048u, o + 3072u);
+      nx = grab_unit(l, units);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc ^= W[i];
+    if (l == 0u) out32[cur] = acc;
+    stored_prev = true;
+    if (s >= count) break;
+  }
+}
+#endif
+
 }  // namespace lk
 }  // namespace wipdb
 

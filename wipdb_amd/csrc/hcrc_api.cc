@@ -51,6 +51,8 @@ __global__ void crc32c_lds_packed_kernel(const uint8_t*, const uint64_t*, const 
                                          uint32_t, unsigned int*);
 __global__ void crc32c_ps_index_kernel(const uint64_t*, const uint32_t*, uint64_t, uint32_t,
                                        uint32_t*, uint32_t*, uint32_t);
+__global__ void crc32c_dma_ceiling_kernel(const uint8_t*, uint64_t, uint32_t*, uint64_t,
+                                          const uint8_t*);
 template <int G, int OUT>
 __global__ void crc32c_lds_list_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                        const uint32_t*, const uint32_t*, const uint32_t*, void*,
@@ -1142,6 +1144,7 @@ int hcrc_ctx_create(int device, hcrc_ctx** out_ctx) {
       reinterpret_cast<const void*>(lk::crc32c_lds_verify_kernel),
       reinterpret_cast<const void*>(lk::crc32c_lds_packed_kernel<0>),
       reinterpret_cast<const void*>(lk::crc32c_lds_packed_kernel<1>),
+      reinterpret_cast<const void*>(lk::crc32c_dma_ceiling_kernel),
       reinterpret_cast<const void*>(lk::crc32c_lds_list_kernel<1, 0>),
       reinterpret_cast<const void*>(lk::crc32c_lds_list_kernel<2, 0>),
       reinterpret_cast<const void*>(lk::crc32c_lds_list_kernel<4, 0>),
@@ -1306,6 +1309,20 @@ int hcrc_readstream_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride, ui
   hipLaunchKernelGGL(wipdb::util::readstream_kernel, dim3(ctx->num_cu), dim3(1024), 0,
                      static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(d_base), stride,
                      length, d_out, static_cast<uint64_t>(count));
+  return Launched();
+}
+
+int hcrc_dma_ceiling_async(hcrc_ctx* ctx, const void* d_base, uint64_t stride, uint32_t length,
+                           uint32_t* d_out, size_t count, void* stream) {
+  if (!ctx || (count && (!d_base || !d_out)) || length != 4096u || stride < 4096u ||
+      count > kMaxLaunchSpans)
+    return HCRC_ERR_INVALID;
+  if (count == 0) return HCRC_OK;
+  HCRC_DEVICE(ctx);
+  hipLaunchKernelGGL(lk::crc32c_dma_ceiling_kernel, dim3(LdsGrid(ctx, count)), dim3(lk::kThreads),
+                     lk::kLdsBytes, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(d_base), stride, d_out,
+                     static_cast<uint64_t>(count), ctx->d_image);
   return Launched();
 }
 
