@@ -227,6 +227,21 @@ int hcrc_ctx_check(hcrc_ctx* ctx);
  * since that stream's last check (the check clears it). */
 int hcrc_sync(hcrc_ctx* ctx, void* stream);
 
+/* Release what the context keeps for `stream`: its fault word (returned to
+ * the free list -- a stream created later, even one HIP hands the same
+ * handle, starts clean) and its HCRC_PACKED pre-pass scratch.  Call it once
+ * the stream's launches are complete (after hcrc_sync or the caller's own
+ * synchronisation) and before the stream is destroyed.  Returns
+ * HCRC_ERR_KERNEL if the stream's word held an unread fault (read and
+ * cleared here, as hcrc_sync would), else HCRC_OK; forgetting a stream the
+ * context never launched on is a no-op.  Without it a context keeps one word
+ * per stream it has seen: past 1024 streams the others share word 0 (a fault
+ * is then reported to every stream past the table: conservative, never
+ * silent) and their packed batches take the default path.
+ * hipStreamPerThread stands for a different queue on every host thread: its
+ * packed batches take the default path, and its threads share one word. */
+int hcrc_stream_forget(hcrc_ctx* ctx, void* stream);
+
 /* Host-memory batch sharded over `ndev` devices by bytes, one host thread
  * and context per device; results land in disjoint slices of out_crcs. */
 int hcrc_batch_multi(const int* devices, int ndev, const void* base,

@@ -62,29 +62,34 @@ PRECONDITION_S = 0.08  # bench.py's power-transient preconditioning
 def time_kernel(fn, stream, reps, windows=2):
     """Average launch time of fn on `stream` over `reps` back-to-back
     launches, the best of `windows` such windows, after untimed launches
-    worth PRECONDITION_S of GPU time (the first ~30-60 ms of back-to-back
-    launches after idle run slow while the SMU settles the clocks, bench.py;
+    worth >= PRECONDITION_S of GPU time (the first ~30-60 ms of back-to-back
+    launches after idle run slow while the SMU raises the clocks, bench.py;
     a single window right after a large allocation and fill once read 26 %
     slow on a box that timed the same batch at its usual rate again a minute
-    later, profiles/r05z_bench.log vs r05z_tbl.log)."""
+    later, profiles/r05z_bench.log vs r05z_tbl.log).  The preconditioning
+    launches and the windows are queued back to back with no host wait
+    between them: a host pause of >= 2 ms lets the memory clocks drop again
+    and the next ~20 launches run 5-18 % slow (profiles/r06a_gap_*.log)."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
+    s.record(stream)
+    fn()
+    e.record(stream)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < PRECONDITION_S:
-        for _ in range(4):
-            fn()
-        torch.cuda.synchronize()
-    best = None
+    one = max(s.elapsed_time(e) / 1e3, 1e-6)
+    n = int(min(4096, max(8, PRECONDITION_S / one + 1)))
+    for _ in range(n):
+        fn()
+    ev = []
     for _ in range(max(1, windows)):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record(stream)
         for _ in range(reps):
             fn()
         e.record(stream)
-        torch.cuda.synchronize()
-        t = s.elapsed_time(e) / reps / 1e3
-        best = t if best is None else min(best, t)
-    return best
+        ev.append((s, e))
+    torch.cuda.synchronize()
+    return min(s.elapsed_time(e) / reps / 1e3 for s, e in ev)
 
 
 def usable_cpus() -> int:

@@ -912,8 +912,9 @@ def test_packed_prepass_verdicts():
     words of the last packed launch).  Packed shapes -- 512 B..2 KiB, table
     blocks, aligned 4 KiB, 64 KiB spans, short / empty spans among them --
     are streamed (meta[0] == 0); unsorted, overlapping, a 5 KiB gap, dense
-    few-byte spans and runs of spans under the stream minimum (WAL records)
-    fall back with the matching kPsBad* bit."""
+    few-byte spans, runs of spans under the stream minimum (WAL records) and
+    a ~4 GiB span past its chunk's first page fall back with the matching
+    kPsBad* bit."""
     assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
     code = (
         "import ctypes, json, numpy as np, torch\n"
@@ -940,6 +941,9 @@ def test_packed_prepass_verdicts():
         "cases['dense'] = lay(20000, 5, 60, 7)\n"
         "cases['wal'] = lay(20000, 40, 95, 7)\n"
         "cases['wal64'] = lay(20000, 64, 127, 7)\n"
+        "o, l = lay(20, 600, 800, 5)\n"
+        "l[10] = 2**32 - 64; o[11:] += np.uint64(2**32)\n"
+        "cases['huge'] = (o, l)\n"
         "cases['again'] = cases['512-2k']\n"
         "res = {}\n"
         "with Engine(0) as eng:\n"
@@ -948,11 +952,13 @@ def test_packed_prepass_verdicts():
         "    for k, (o, l) in cases.items():\n"
         "        do = torch.from_numpy(o.view(np.int64)).cuda()\n"
         "        dl = torch.from_numpy(l.view(np.int32)).cuda()\n"
-        "        eng.batch_device(d, do, dl, packed=True)\n"
+        "        out = eng.batch_device(d, do, dl, packed=True)\n"
         "        torch.cuda.synchronize()\n"
         "        m = (ctypes.c_uint32 * 8)()\n"
         "        lib.hcrc_test_packed_meta(m, 8)\n"
         "        res[k] = [int(x) for x in m]\n"
+        "        if k == 'huge':  # (the ~4 GiB span: the same CRCs as the default path)\n"
+        "            assert bool((out == eng.batch_device(d, do, dl)).all())\n"
         "print('META ' + json.dumps(res))\n")
     env = dict(os.environ, PYTHONPATH=REPO, WIPDB_HCRC_LIB=TEST_LIB)
     env.pop("WIPDB_HCRC_FORCE_FAULT", None)
@@ -970,6 +976,9 @@ def test_packed_prepass_verdicts():
     for k in ("unsorted", "overlap", "gap5k"):
         assert res[k][0] & 1, (k, res[k])
     assert res["dense"][0] & 2, res["dense"]
+    # a ~4 GiB span not on its chunk's first page would wrap
+    # run_ps's 32-bit positions -- the pre-pass sends it to the default path
+    assert res["huge"][0] & 1, res["huge"]
     assert res["wal"][0] & 4, res["wal"]  # runs of short spans (kPsBadShort)
     assert res["wal64"][0] & 4, res["wal64"]  # half of them short
 
@@ -1469,6 +1478,73 @@ def test_kernel_fault_stays_with_its_stream():
     r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "stream faults ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
+
+
+def test_stream_forget_releases_words():
+    """ADVICE / VERDICT r5: stream-keyed state is released.  Test build: a
+    forced fault on stream A is returned by hcrc_stream_forget (and only
+    once); 1100 streams are then created, used, synchronised, forgotten and
+    destroyed (HIP reuses their handles), and afterwards a fault on a new
+    stream D still reaches D alone -- had the 1024-word table run out, D and
+    the healthy stream E would share word 0 and E would report it.  A packed
+    batch on hipStreamPerThread (which is another queue on every thread)
+    takes the default path and is correct."""
+    assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
+    code = (
+        "import numpy as np, torch, gc\n"
+        "from wipdb_amd import Engine, HcrcError, _lib\n"
+        "import sys; sys.path.insert(0, 'tests')\n"
+        "lib = _lib.load()\n"
+        "rng = np.random.default_rng(8)\n"
+        "n = 3000\n"
+        "lens = rng.integers(96, 1000, n).astype(np.uint32)\n"
+        "offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 5)[:-1]]).astype(np.uint64)\n"
+        "buf = rng.integers(0, 256, int(offs[-1]) + 1100, dtype=np.uint8)\n"
+        "def rc_of(f):\n"
+        "    try:\n"
+        "        f()\n"
+        "        return 0\n"
+        "    except HcrcError as e:\n"
+        "        return e.code\n"
+        "with Engine(0) as eng:\n"
+        "    want = eng.batch(buf, offs, lens)\n"
+        "    d = torch.from_numpy(buf).cuda()\n"
+        "    do = torch.from_numpy(offs.view(np.int64)).cuda()\n"
+        "    dl = torch.from_numpy(lens.view(np.int32)).cuda()\n"
+        "    sa = torch.cuda.Stream()\n"
+        "    lib.hcrc_test_force_fault(1)\n"
+        "    eng.batch_device(d, do, dl, stream=sa.cuda_stream)\n"
+        "    lib.hcrc_test_force_fault(0)\n"
+        "    sa.synchronize()\n"
+        "    assert rc_of(lambda: eng.stream_forget(sa.cuda_stream)) == _lib.HCRC_ERR_KERNEL\n"
+        "    assert rc_of(lambda: eng.stream_forget(sa.cuda_stream)) == 0\n"
+        "    del sa; gc.collect()\n"
+        "    for i in range(1100):\n"
+        "        s = torch.cuda.Stream()\n"
+        "        out = eng.batch_device(d, do, dl, stream=s.cuda_stream, packed=(i % 2 == 0))\n"
+        "        eng.sync(s.cuda_stream)\n"
+        "        eng.stream_forget(s.cuda_stream)\n"
+        "        if i % 97 == 0:\n"
+        "            assert (out.cpu().numpy().view(np.uint32) == want).all(), i\n"
+        "        del s, out\n"
+        "    sd, se = torch.cuda.Stream(), torch.cuda.Stream()\n"
+        "    lib.hcrc_test_force_fault(1)\n"
+        "    eng.batch_device(d, do, dl, stream=sd.cuda_stream)\n"
+        "    lib.hcrc_test_force_fault(0)\n"
+        "    eng.batch_device(d, do, dl, stream=se.cuda_stream)\n"
+        "    assert rc_of(lambda: eng.sync(se.cuda_stream)) == 0\n"
+        "    assert rc_of(lambda: eng.sync(sd.cuda_stream)) == _lib.HCRC_ERR_KERNEL\n"
+        "    per_thread = 2  # hipStreamPerThread\n"
+        "    out = eng.batch_device(d, do, dl, stream=per_thread, packed=True)\n"
+        "    eng.sync(per_thread)\n"
+        "    assert (out.cpu().numpy().view(np.uint32) == want).all()\n"
+        "    assert lib.hcrc_ctx_check(eng._ctx) == _lib.HCRC_OK\n"
+        "print('stream forget ok')\n")
+    env = dict(os.environ, PYTHONPATH=REPO, WIPDB_HCRC_LIB=TEST_LIB, WIPDB_PS_MIN_SPANS="0")
+    env.pop("WIPDB_HCRC_FORCE_FAULT", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "stream forget ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
 
 
 def test_no_fault_in_healthy_launches(engine):

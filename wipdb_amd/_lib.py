@@ -59,6 +59,7 @@ _PROTOS = {
     "hcrc_verify_async_ex": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _c.c_int, _vp]),
     "hcrc_sync": (_c.c_int, [_vp, _vp]),
     "hcrc_ctx_check": (_c.c_int, [_vp]),
+    "hcrc_stream_forget": (_c.c_int, [_vp, _vp]),
     "hcrc_batch_multi": (
         _c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _vp, _vp, _vp, _vp, _vp, _sz, _c.c_int]),
     "hcrc_batch_multi_ex": (

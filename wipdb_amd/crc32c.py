@@ -323,6 +323,14 @@ class Engine:
         fault since the stream's last check."""
         check(self._lib.hcrc_sync(self._ctx, self._stream_of(stream)), "hcrc_sync")
 
+    def stream_forget(self, stream) -> None:
+        """hcrc_stream_forget: release this context's fault word and packed
+        scratch for ``stream`` once its launches are complete, before the
+        stream is destroyed; raises HCRC_ERR_KERNEL if its word held an
+        unread fault."""
+        check(self._lib.hcrc_stream_forget(self._ctx, self._stream_of(stream)),
+              "hcrc_stream_forget")
+
 
 def batch_multi(devices: Sequence[int], base, offsets, lengths, inits=None,
                 mask_output: bool = False, shard_status: bool = False):

@@ -188,6 +188,12 @@ __device__ __forceinline__ void ps_index(const uint8_t* base, const uint64_t* of
           if (cp > c) cp = c;
         }
         for (uint64_t k = cp + 1u; k <= c; ++k) first[k] = static_cast<uint32_t>(i);
+        // run_ps keeps a chunk's positions in 32 bits from the page of its
+        // first span (W0 >= the chunk's start - 4095): a span starting in the
+        // chunk ends before W0 + cb + 4096 + len, rounded up to a page -- it
+        // must stay below 2^32 (a span of ~4 GiB not on the
+        // chunk's first page would wrap)
+        if (cb + L[j] + 8192u >= (uint64_t(1) << 32)) bad |= kPsBad;
         if (i + kPsDense < n && AD[j] - a < 4096u) bad |= kPsBadDense;
         if (i + kPsDense < n && AD[j] < a) bad |= kPsBad;
         if (i == n - 1)

@@ -290,6 +290,8 @@ struct hcrc_ctx {
   unsigned int* d_fault_words = nullptr;
   std::mutex faults_mu;
   std::map<hipStream_t, uint32_t> stream_words;
+  uint32_t stream_words_next = 0;        // words handed out so far (of kStreamFaultWords)
+  std::vector<uint32_t> free_stream_words;  // returned by hcrc_stream_forget
   // HCRC_PACKED's pre-pass output per stream (meta words + the chunk index),
   // kept across launches: the verdict word is tagged with the stream's
   // launch count, so nothing is cleared or allocated per call
@@ -579,8 +581,15 @@ unsigned int* StreamFaultWord(hcrc_ctx* ctx, hipStream_t st) {
   std::lock_guard<std::mutex> lk(ctx->faults_mu);
   auto it = ctx->stream_words.find(st);
   if (it != ctx->stream_words.end()) return ctx->d_fault_words + it->second;
-  if (ctx->stream_words.size() >= kStreamFaultWords) return ctx->d_fault_words;
-  const uint32_t k = 1u + kMaxLanes + static_cast<uint32_t>(ctx->stream_words.size());
+  uint32_t k;
+  if (!ctx->free_stream_words.empty()) {  // (a forgotten stream's word, cleared then)
+    k = ctx->free_stream_words.back();
+    ctx->free_stream_words.pop_back();
+  } else if (ctx->stream_words_next < kStreamFaultWords) {
+    k = 1u + kMaxLanes + ctx->stream_words_next++;
+  } else {
+    return ctx->d_fault_words;
+  }
   ctx->stream_words.emplace(st, k);
   return ctx->d_fault_words + k;
 }
@@ -595,7 +604,9 @@ hcrc_ctx::PsScratch* PsScratchFor(hcrc_ctx* ctx, hipStream_t st, size_t words) {
   if (ctx->ps_scratch.size() >= kPsStreams) return nullptr;
   auto ps = std::make_unique<hcrc_ctx::PsScratch>();
   if (hipMalloc(reinterpret_cast<void**>(&ps->d), words * 4) != hipSuccess) return nullptr;
-  if (hipMemset(ps->d, 0, words * 4) != hipSuccess) {
+  // the verdict words only, ordered on the caller's stream ahead of its first
+  // pre-pass (first[] is written by every pre-pass before it is read)
+  if (hipMemsetAsync(ps->d, 0, lk::kPsMetaWords * 4, st) != hipSuccess) {
     (void)hipFree(ps->d);
     return nullptr;
   }
@@ -643,8 +654,11 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
       }();
       // the stream's pre-pass scratch (none: past kPsStreams streams or out
       // of memory -- the batch takes the default path)
+      // (hipStreamPerThread is another queue on every host thread: a scratch
+      // keyed by it would be shared between queues, so its batches take the
+      // default path -- ADVICE r5)
       hcrc_ctx::PsScratch* const ps =
-          (flags & HCRC_PACKED) && n >= packed_min
+          (flags & HCRC_PACKED) && n >= packed_min && st != hipStreamPerThread
               ? PsScratchFor(ctx, st, size_t(chunks_per_group) * ctx->num_cu + 1 + lk::kPsMetaWords)
               : nullptr;
       if (ps) {
@@ -1407,6 +1421,37 @@ int hcrc_sync(hcrc_ctx* ctx, void* stream) {
     any = __atomic_exchange_n(ctx->fault_words + it->second, 0u, __ATOMIC_SEQ_CST);
   else if (ctx->stream_words.size() >= kStreamFaultWords)
     any = __atomic_exchange_n(ctx->fault_words, 0u, __ATOMIC_SEQ_CST);
+  return any ? HCRC_ERR_KERNEL : HCRC_OK;
+}
+
+int hcrc_stream_forget(hcrc_ctx* ctx, void* stream) {
+  if (!ctx) return HCRC_ERR_INVALID;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  unsigned int any = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx->faults_mu);
+    const auto it = ctx->stream_words.find(st);
+    if (it != ctx->stream_words.end()) {
+      any = __atomic_exchange_n(ctx->fault_words + it->second, 0u, __ATOMIC_SEQ_CST);
+      ctx->free_stream_words.push_back(it->second);
+      ctx->stream_words.erase(it);
+    }
+  }
+  std::unique_ptr<hcrc_ctx::PsScratch> ps;
+  {
+    std::lock_guard<std::mutex> lk(ctx->ps_mu);
+    const auto it = ctx->ps_scratch.find(st);
+    if (it != ctx->ps_scratch.end()) {
+      ps = std::move(it->second);
+      ctx->ps_scratch.erase(it);
+    }
+  }
+  if (ps && ps->d) {
+    HCRC_DEVICE(ctx);
+    // (the caller's launches on the stream are complete; hipFree waits for
+    // the device anyway)
+    if (hipFree(ps->d) != hipSuccess) return HCRC_ERR_HIP;
+  }
   return any ? HCRC_ERR_KERNEL : HCRC_OK;
 }
 
