@@ -327,10 +327,14 @@ void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std:
   static_assert(kThreads == kPsIndexThreads, "emu::launch runs kThreads lanes a workgroup");
   const uint32_t pgrid = static_cast<uint32_t>(std::min<size_t>((n + kPsIndexThreads - 1) / kPsIndexThreads, 8));
   emu::launch(pgrid ? pgrid : 1, [&] {
-    crc32c_ps_index_kernel(offs.data(), lens.data(), n, C, first.data(), meta.data(), kEpoch);
+    crc32c_ps_index_kernel(data, offs.data(), lens.data(), n, C, first.data(), meta.data(), kEpoch,
+                           g_packed_flags);
   });
-  const bool packed = meta[0] == kEpoch << 4;
-  if (packed)
+  // this launch's verdict, nothing broken; kPsEa: the batch suits run_ea,
+  // which the packed kernel takes without the index (none was written)
+  const bool ea_only = meta[0] == (kEpoch << 4 | kPsEa);
+  const bool packed = meta[0] == kEpoch << 4 || ea_only;
+  if (packed && !ea_only)
     for (uint32_t c = 0; c <= C; ++c)
       if (first[c] > n || (c && first[c] < first[c - 1])) {
         fprintf(stderr, "  %s: first[%u] = %u\n", name, c, first[c]);

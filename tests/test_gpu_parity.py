@@ -909,9 +909,10 @@ def test_packed_stream_only_matches_default():
 
 def test_packed_prepass_verdicts():
     """Which pipeline a HCRC_PACKED batch takes (test build: the pre-pass's
-    words of the last packed launch).  Packed shapes -- 512 B..2 KiB, table
-    blocks, aligned 4 KiB, 64 KiB spans, short / empty spans among them --
-    are streamed (meta[0] == 0); unsorted, overlapping, a 5 KiB gap, dense
+    words of the last packed launch).  Packed shapes -- 512 B..2 KiB, short
+    / empty spans among them -- are streamed (meta[0] == 0); table blocks,
+    aligned 4 KiB and 64 KiB spans suit run_ea, and the pre-pass stops after
+    its sample (kPsEa, 8); unsorted, overlapping, a 5 KiB gap, dense
     few-byte spans, runs of spans under the stream minimum (WAL records) and
     a ~4 GiB span past its chunk's first page fall back with the matching
     kPsBad* bit."""
@@ -970,9 +971,12 @@ def test_packed_prepass_verdicts():
     print(res)
     # ("again": a packed batch after four broken ones on the same lanes:
     # each launch's verdict is its own, not a leftover)
-    for k in ("512-2k", "tblocks", "a4k", "b65536", "shorts", "again"):
+    for k in ("512-2k", "shorts", "again"):
         assert res[k][0] == 0, (k, res[k])
         assert res[k][1] % 4096 == 0 and res[k][1] >= 4096, (k, res[k])
+    # batches that suit run_ea: the pre-pass stops after its sample (kPsEa)
+    for k in ("tblocks", "a4k", "b65536"):
+        assert res[k][0] == 8, (k, res[k])
     for k in ("unsorted", "overlap", "gap5k"):
         assert res[k][0] & 1, (k, res[k])
     assert res["dense"][0] & 2, res["dense"]

@@ -119,6 +119,9 @@ constexpr uint32_t kPsBad = 1u, kPsBadDense = 2u;
 // memory; a run of 8 of them, or 32 among a step's 64 spans (WAL records),
 // sends the batch to the lane-packed pipeline instead
 constexpr uint32_t kPsBadShort = 4u;
+// not indexed: the batch suits run_ea (pick_ea), which the packed kernel takes
+// without reading the index -- the pre-pass stops after its sample
+constexpr uint32_t kPsEa = 8u;
 // the pre-pass kernel's workgroup (16 waves: one verdict atomic per 1024
 // threads) and its LDS (a word per wave)
 constexpr uint32_t kPsIndexThreads = 1024;

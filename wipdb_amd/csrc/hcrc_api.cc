@@ -49,8 +49,8 @@ __global__ void crc32c_lds_packed_kernel(const uint8_t*, const uint64_t*, const 
                                          const uint32_t*, uint32_t*, uint64_t, uint32_t,
                                          const uint8_t*, const uint32_t*, const uint32_t*, uint32_t,
                                          uint32_t, unsigned int*);
-__global__ void crc32c_ps_index_kernel(const uint64_t*, const uint32_t*, uint64_t, uint32_t,
-                                       uint32_t*, uint32_t*, uint32_t);
+__global__ void crc32c_ps_index_kernel(const uint8_t*, const uint64_t*, const uint32_t*, uint64_t,
+                                       uint32_t, uint32_t*, uint32_t*, uint32_t, uint32_t);
 __global__ void crc32c_dma_ceiling_kernel(const uint8_t*, uint64_t, uint32_t*, uint64_t,
                                           const uint8_t*);
 template <int G, int OUT>
@@ -680,8 +680,9 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
             1, std::min<size_t>((n + lk::kPsIndexThreads - 1) / lk::kPsIndexThreads,
                                 size_t(ctx->num_cu) * 2)));
         hipLaunchKernelGGL(lk::crc32c_ps_index_kernel, dim3(pgrid), dim3(lk::kPsIndexThreads),
-                           lk::kPsIndexLds, st, off + pos,
-                           len + pos, static_cast<uint64_t>(n), C, first, meta, ps->epoch);
+                           lk::kPsIndexLds, st, static_cast<const uint8_t*>(base), off + pos,
+                           len + pos, static_cast<uint64_t>(n), C, first, meta, ps->epoch,
+                           ps_only ? lk::kFlagPsOnly : 0u);
 #ifdef WIPDB_HCRC_TEST_HOOKS
         // (test build: the pre-pass's verdict and chunk size, for the tests
         // that check which pipeline a packed batch took; word 0 as the
