@@ -28,8 +28,8 @@ import time
 import numpy as np
 import torch
 
-from scripts.bench_extra import (BUCKETS, batch_latency, dev, pcie_h2d_ceiling, sst_layout,
-                                 time_kernel, zipf_spans)
+from scripts.bench_extra import (BUCKETS, batch_latency, dev, host_batch_latency,
+                                 pcie_h2d_ceiling, sst_layout, time_kernel, zipf_spans)
 
 HBM_PEAK_BYTES = 8.0e12
 
@@ -121,6 +121,9 @@ def run_tables(eng, d, stream, ref_fn, rng, gib=4.0):
     tb["packed"] = _rate(float(lens.sum()), tp)
     tb["packed"]["kernel_ms"] = round(tp * 1e3, 4)
     tb["packed"]["same_as_default"] = bool((outp == out).all())
+    # per-SST latency (BuildTableKV's batch, kv/src/db/builder.cc:18-109):
+    # ~2 MiB of these blocks a call, device-resident through the C-ABI
+    tb["latency_2MiB_device"] = batch_latency(eng, data, do, dl, stream)
     torch.cuda.synchronize()
     tb["parity"] = _ref_check(ref_fn, data.cpu().numpy(), offs, lens,
                               out.cpu().numpy().view(np.uint32), rng)
@@ -159,6 +162,8 @@ def run_config5(eng, ref_fn, rng, n_sst=256):
         host = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(pin.value))
         host[:] = rng.integers(32, 127, nbytes, dtype=np.uint8)
         eng.batch(host, offs[:1000], lens[:1000])
+        # one SST's blocks a call (the product's per-flush hcrc_batch, zero-copy)
+        lat = host_batch_latency(eng, pin.value, offs, lens)
         reps = 5
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -173,6 +178,7 @@ def run_config5(eng, ref_fn, rng, n_sst=256):
                 "GiBps_end_to_end": round(rate, 2), "pcie_h2d_ceiling_GiBps": ceiling,
                 "fraction_of_pcie_ceiling": round(rate / ceiling, 3),
                 "timing": "host wall time of %d synchronous calls" % reps,
+                "latency_2MiB_sst": lat,
                 "parity": _ref_check(ref_fn, host, offs, lens, got, rng, mask=True)}
     finally:
         lib.hcrc_host_free(pin)

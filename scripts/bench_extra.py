@@ -132,21 +132,55 @@ NO_CPU = False  # --no-cpu: skip the CPU rates (same-session A/B runs)
 
 def batch_latency(eng, dbuf, do, dl, stream, nbatch_bytes=2 << 20, reps=200):
     """p50 / p99 of synchronised SST-sized batches (~2 MiB of these spans per
-    launch, consecutive slices of the batch), host wall time."""
+    launch, consecutive slices of the batch), host wall time from the launch
+    call to the synchronize's return.  The launch goes through the C-ABI
+    (hcrc_batch_async by ctypes, as a C++ caller would make it; the Python
+    wrapper's argument checks cost ~10 us a call, profiles/r06g_latency.log)."""
+    from wipdb_amd import _lib
     lens = dl.cpu().numpy().view(np.uint32).astype(np.int64)
     per = max(1, int(np.searchsorted(np.cumsum(lens + 5), nbatch_bytes)))
     n = lens.size
     outs = torch.empty(per, dtype=torch.int32, device=dbuf.device)
+    flags = (_lib.HCRC_DEVICE_PTRS | (_lib.HCRC_SPLIT_SMALL if SPLIT else 0)
+             | (_lib.HCRC_SPLIT_LONG if SPLIT_LONG else 0))
+    lib, ctx, sp = eng._lib, eng._ctx, stream.cuda_stream
     lat = []
     for i in range(reps + 20):
         lo = (i * per) % max(1, n - per)
-        o_i, l_i = do[lo:lo + per], dl[lo:lo + per]
+        cnt = min(per, n - lo)
+        a_off, a_len = do.data_ptr() + 8 * lo, dl.data_ptr() + 4 * lo
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.batch_device(dbuf, o_i, l_i, None, outs, stream=stream.cuda_stream, split_small=SPLIT,
-                         split_long=SPLIT_LONG)
+        rc = lib.hcrc_batch_async(ctx, dbuf.data_ptr(), a_off, a_len, None, outs.data_ptr(), cnt,
+                                  flags, sp)
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t0)
+        _lib.check(rc, "hcrc_batch_async")
+    lat = np.array(lat[20:]) * 1e6
+    return {"spans_per_batch": int(min(per, n)), "p50_us": round(float(np.percentile(lat, 50)), 1),
+            "p99_us": round(float(np.percentile(lat, 99)), 1)}
+
+
+def host_batch_latency(eng, host_ptr, offs, lens, nbatch_bytes=2 << 20, reps=200):
+    """The same for the product's own per-SST call: hcrc_batch on host
+    pointers (a TableBuilder write buffer in pinned memory: zero-copy), ~2 MiB
+    of spans a call, synchronous."""
+    from wipdb_amd import _lib
+    per = max(1, int(np.searchsorted(np.cumsum(lens.astype(np.int64) + 5), nbatch_bytes)))
+    n = offs.size
+    out = np.empty(per, np.uint32)
+    lib, ctx = eng._lib, eng._ctx
+    lat = []
+    for i in range(reps + 20):
+        lo = (i * per) % max(1, n - per)
+        cnt = min(per, n - lo)
+        o = offs[lo:lo + cnt]
+        ln = lens[lo:lo + cnt]
+        t0 = time.perf_counter()
+        rc = lib.hcrc_batch(ctx, host_ptr, o.ctypes.data, ln.ctypes.data, None, out.ctypes.data,
+                            cnt, _lib.HCRC_MASK_OUTPUT)
+        lat.append(time.perf_counter() - t0)
+        _lib.check(rc, "hcrc_batch")
     lat = np.array(lat[20:]) * 1e6
     return {"spans_per_batch": int(min(per, n)), "p50_us": round(float(np.percentile(lat, 50)), 1),
             "p99_us": round(float(np.percentile(lat, 99)), 1)}

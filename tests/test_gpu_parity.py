@@ -873,8 +873,9 @@ def test_packed_stream_only_matches_default():
     table blocks, spans of >= 16 KiB) to it; with WIPDB_PS_ONLY=1 run_ps takes
     them too.  Those shapes through run_ps -- and spans of 1..9 MiB, a
     register carried over thousands of pages -- with inits and the masked
-    output, equal the default pipeline's CRCs (itself checked against the
-    oracle above), over a few hundred MiB each."""
+    output, equal the default pipeline's CRCs over a few hundred MiB each,
+    and a sample of 300 spans per case and mode equals the compiled
+    reference's (oracle/_ref; the oracle restatement where it is absent)."""
     code = (
         "import numpy as np, torch\n"
         "from wipdb_amd import Engine\n"
@@ -887,19 +888,34 @@ def test_packed_stream_only_matches_default():
         "         'b16k': lay(15000, 16384, 18432, 0, 1),\n"
         "         'mib': lay(40, 1 << 20, 9 << 20, 3, 5)}\n"
         "bad = []\n"
+        "import ctypes, sys\n"
+        "sys.path.insert(0, 'tests')\n"
+        "from conftest import Reference, REF_SO, Oracle\n"
+        "import os\n"
+        "ref = Reference() if os.path.exists(REF_SO) else Oracle()\n"
+        "checked = 0\n"
         "with Engine(0) as eng:\n"
         "    size = max(int((o + l).max()) for o, l in cases.values()) + 64\n"
         "    d = torch.randint(0, 256, (size,), dtype=torch.uint8, device='cuda')\n"
+        "    host = d.cpu().numpy()\n"
         "    for k, (o, l) in cases.items():\n"
         "        do = torch.from_numpy(o.view(np.int64)).cuda()\n"
         "        dl = torch.from_numpy(l.view(np.int32)).cuda()\n"
-        "        di = torch.from_numpy(rng.integers(0, 2**32, o.size, dtype=np.uint64).astype(np.uint32).view(np.int32)).cuda()\n"
+        "        iv = rng.integers(0, 2**32, o.size, dtype=np.uint64).astype(np.uint32)\n"
+        "        di = torch.from_numpy(iv.view(np.int32)).cuda()\n"
         "        for inits, m in ((None, False), (di, True)):\n"
         "            a = eng.batch_device(d, do, dl, inits, mask_output=m, packed=True)\n"
         "            b = eng.batch_device(d, do, dl, inits, mask_output=m)\n"
         "            if not bool((a == b).all()):\n"
         "                bad.append((k, m, int((a != b).sum())))\n"
-        "print('BAD', bad)\n")
+        "            # run_ps itself against the reference (oracle/_ref) on a sample\n"
+        "            idx = np.sort(rng.choice(o.size, min(o.size, 300), replace=False))\n"
+        "            want = ref.batch(host, o[idx], l[idx], None if inits is None else iv[idx], mask=m)\n"
+        "            got = a.cpu().numpy().view(np.uint32)[idx]\n"
+        "            checked += idx.size\n"
+        "            if not (got == want).all():\n"
+        "                bad.append((k, m, 'ref', int((got != want).sum())))\n"
+        "print('BAD', bad, 'REF_CHECKED', checked)\n")
     env = dict(os.environ, PYTHONPATH=REPO, WIPDB_PS_ONLY="1", WIPDB_PS_CHUNKS="16")
     r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
                        text=True, timeout=300)
