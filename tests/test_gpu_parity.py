@@ -1003,6 +1003,80 @@ def test_packed_prepass_verdicts():
     assert res["wal64"][0] & 4, res["wal64"]  # half of them short
 
 
+def test_host_batches_take_the_host_index():
+    """host batches (hcrc_batch, what ExtendBatch ->
+    FinishTables / VerifyTables / WriteLog reach) check the packing promise
+    and build the chunk index on the host (HostPsIndex), then launch the
+    packed kernel with no pre-pass and no 32 Ki-span floor.  Test build: the
+    last packed launch's words say the index was the host's.  Staged
+    (pageable) pieces are packed by construction; zero-copy pieces keep the
+    caller's layout, so an unsorted one takes the default kernel.  Every CRC
+    (inits, masked) against the oracle."""
+    assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
+    code = (
+        "import ctypes, json, sys, numpy as np\n"
+        "sys.path.insert(0, 'tests')\n"
+        "from conftest import Oracle\n"
+        "from wipdb_amd import Engine, _lib\n"
+        "lib = _lib.load()\n"
+        "ora = Oracle()\n"
+        "rng = np.random.default_rng(21)\n"
+        "def lay(n, lo, hi, g, start=3):\n"
+        "    l = rng.integers(lo, hi + 1, n).astype(np.uint64)\n"
+        "    return start + np.concatenate([[0], np.cumsum(l + g)[:-1]]).astype(np.uint64), l.astype(np.uint32)\n"
+        "cases = {'short': lay(20000, 512, 2200, 5), 'tblocks': lay(6000, 4097, 4225, 4, 0),\n"
+        "         'wal': lay(20000, 40, 95, 7)}\n"
+        "o, l = lay(9000, 300, 3000, 5)\n"
+        "o[[10, 11]] = o[[11, 10]]\n"
+        "cases['unsorted'] = (o, l)\n"
+        "size = max(int((o + l).max()) for o, l in cases.values()) + 64\n"
+        "res, bad = {}, []\n"
+        "with Engine(0) as eng:\n"
+        "    pin = ctypes.c_void_p()\n"
+        "    _lib.check(lib.hcrc_host_alloc(size, ctypes.byref(pin)), 'alloc')\n"
+        "    pinned = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(pin.value))\n"
+        "    pageable = rng.integers(0, 256, size, dtype=np.uint8)\n"
+        "    pinned[:] = pageable\n"
+        "    for k, (o, l) in cases.items():\n"
+        "        iv = rng.integers(0, 2**32, o.size, dtype=np.uint64).astype(np.uint32)\n"
+        "        for where, buf in (('staged', pageable), ('zerocopy', pinned)):\n"
+        "            for inits, m in ((None, False), (iv, True)):\n"
+        "                lib.hcrc_test_clear_packed_meta()\n"
+        "                got = eng.batch(buf, o, l, inits, mask_output=m)\n"
+        "                meta = (ctypes.c_uint32 * 8)()\n"
+        "                lib.hcrc_test_packed_meta(meta, 8)\n"
+        "                res[f'{k}/{where}/{int(m)}'] = [int(meta[0]), int(meta[7])]\n"
+        "                want = ora.batch(pageable, o, l, inits, mask=m)\n"
+        "                if not (got == want).all():\n"
+        "                    bad.append((k, where, m, int((got != want).sum())))\n"
+
+        "    lib.hcrc_host_free(pin)\n"
+        "print('META ' + json.dumps(res))\n"
+        "print('BAD', bad)\n")
+    env = dict(os.environ, PYTHONPATH=REPO, WIPDB_HCRC_LIB=TEST_LIB)
+    env.pop("WIPDB_HCRC_FORCE_FAULT", None)
+    env.pop("WIPDB_PS_MIN_SPANS", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "BAD []" in r.stdout, r.stdout[-2000:]
+    import json
+    res = json.loads(r.stdout.split("META ", 1)[1].splitlines()[0])
+    print(res)
+    host = 0x484F5354
+    # the promise holds: the host's index (word 7), verdict 0
+    for k in ("short", "tblocks"):
+        for where in ("staged", "zerocopy"):
+            for m in ("0", "1"):
+                assert res[f"{k}/{where}/{m}"] == [0, host], (k, where, m, res)
+    # the staged copy of an unsorted batch is the slot's own, sorted layout
+    assert res["unsorted/staged/0"] == [0, host], res
+    # zero-copy keeps the caller's unsorted layout, and WAL records stay on
+    # run_lp: no packed launch (the cleared words are left as they were)
+    for k in ("unsorted/zerocopy/0", "wal/zerocopy/0", "wal/staged/0"):
+        assert res[k][1] != host, (k, res)
+
+
 def _run_device_packed(engine, buf, offs, lens):
     out = engine.batch_device(_t(buf), _t(np.asarray(offs, np.uint64)),
                               _t(np.asarray(lens, np.uint32)), packed=True)

@@ -127,6 +127,11 @@ constexpr int kMaxLanes = 8;                      // concurrent synchronous call
 // that, streams share word 0).
 constexpr uint32_t kStreamFaultWords = 1024;
 constexpr uint32_t kFaultWords = 1 + kMaxLanes + kStreamFaultWords;
+// HCRC_PACKED chunks per workgroup (one per wave, progress-balanced;
+// WIPDB_PS_CHUNKS: tuning runs) and the largest grid a host-built index serves
+constexpr int kPsChunksPerGroup = 16;
+constexpr uint32_t kPsMaxHostChunks = 16u * 1024u;
+constexpr size_t kPsHostWords = lk::kPsMetaWords + kPsMaxHostChunks + 1;
 
 // One piece of a host batch in flight: pinned host buffers and their device
 // mirrors.
@@ -136,11 +141,13 @@ struct Slot {
   uint32_t* h_len = nullptr;
   uint32_t* h_init = nullptr;
   uint32_t* h_out = nullptr;
+  uint32_t* h_ps = nullptr;  // pinned: a host-built HCRC_PACKED index (meta words + first[])
   uint8_t* d_data = nullptr;
   uint64_t* d_off = nullptr;
   uint32_t* d_len = nullptr;
   uint32_t* d_init = nullptr;
   uint32_t* d_out = nullptr;
+  uint32_t* d_ps = nullptr;
   size_t cap_bytes = 0;
   hipEvent_t done = nullptr;
   // results still to be copied out to the caller once `done` fires
@@ -153,11 +160,13 @@ struct Slot {
     if (h_len) (void)hipHostFree(h_len);
     if (h_init) (void)hipHostFree(h_init);
     if (h_out) (void)hipHostFree(h_out);
+    if (h_ps) (void)hipHostFree(h_ps);
     if (d_data) (void)hipFree(d_data);
     if (d_off) (void)hipFree(d_off);
     if (d_len) (void)hipFree(d_len);
     if (d_init) (void)hipFree(d_init);
     if (d_out) (void)hipFree(d_out);
+    if (d_ps) (void)hipFree(d_ps);
     if (done) (void)hipEventDestroy(done);
     *this = Slot();
   }
@@ -175,11 +184,13 @@ struct Slot {
     host(reinterpret_cast<void**>(&h_len), kStageSpans * 4);
     host(reinterpret_cast<void**>(&h_init), kStageSpans * 4);
     host(reinterpret_cast<void**>(&h_out), kStageSpans * 4);
+    host(reinterpret_cast<void**>(&h_ps), kPsHostWords * 4);
     dev(reinterpret_cast<void**>(&d_data), kStageBytes);
     dev(reinterpret_cast<void**>(&d_off), kStageSpans * 8);
     dev(reinterpret_cast<void**>(&d_len), kStageSpans * 4);
     dev(reinterpret_cast<void**>(&d_init), kStageSpans * 4);
     dev(reinterpret_cast<void**>(&d_out), kStageSpans * 4);
+    dev(reinterpret_cast<void**>(&d_ps), kPsHostWords * 4);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
     if (e != hipSuccess) {
       Free();
@@ -618,9 +629,30 @@ hcrc_ctx::PsScratch* PsScratchFor(hcrc_ctx* ctx, hipStream_t st, size_t words) {
 // Descriptor batch on device memory, enqueued on st.  auto_long: kDevice for
 // the device entry points (a batch of <= kAutoLongSpans spans splits its long
 // spans by itself); host pieces decide on the host (AutoLongHost).
+// A chunk index the host built for a piece it staged or checked
+// (HostPsIndex): device words [meta (kPsMetaWords) | first[C + 1]], verdict
+// tagged with epoch 1.
+struct HostIndex {
+  const uint32_t* d_ps;
+  uint32_t C;
+};
+
+int PsChunksPerGroup() {
+  static const int v = [] {
+    const char* e = getenv("WIPDB_PS_CHUNKS");  // (tuning: chunks per workgroup)
+    const int c = e ? atoi(e) : 0;
+    return c >= 1 && c <= 1024 ? c : kPsChunksPerGroup;
+  }();
+  return v;
+}
+bool PsOnly() {
+  static const bool v = getenv("WIPDB_PS_ONLY") && atoi(getenv("WIPDB_PS_ONLY")) != 0;
+  return v;
+}
+
 int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint32_t* len,
                 const uint32_t* init, uint32_t* out, size_t count, int flags, hipStream_t st,
-                AutoLong auto_long, unsigned int* fault) {
+                AutoLong auto_long, unsigned int* fault, const HostIndex* hidx = nullptr) {
   const bool mask = (flags & HCRC_MASK_OUTPUT) != 0;
   const bool split_long = (flags & HCRC_SPLIT_LONG) != 0 ||
                           (auto_long == AutoLong::kDevice && (flags & HCRC_SPLIT_SMALL) == 0 &&
@@ -647,11 +679,24 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         const char* e = getenv("WIPDB_PS_MIN_SPANS");
         return e && *e ? static_cast<size_t>(atol(e)) : kPackedMinSpans;
       }();
-      static const int chunks_per_group = [] {
-        const char* e = getenv("WIPDB_PS_CHUNKS");  // (tuning: chunks per workgroup)
-        const int v = e ? atoi(e) : 0;
-        return v >= 1 && v <= 1024 ? v : 16;  // one chunk per wave (progress-balanced)
-      }();
+      const int chunks_per_group = PsChunksPerGroup();
+      const bool ps_only = PsOnly();
+      if (hidx && count <= kMaxLaunchSpans &&
+          hidx->C == static_cast<uint32_t>(chunks_per_group * grid)) {
+        // a piece whose index the host built (HostPsIndex): no pre-pass, no
+        // floor -- the packed kernel's own pick_ea still takes run_ea where
+        // it suits the piece
+        hipLaunchKernelGGL(init ? lk::crc32c_lds_packed_kernel<1> : lk::crc32c_lds_packed_kernel<0>,
+                           dim3(grid), dim3(lk::kThreads), lk::kLdsBytes, st,
+                           static_cast<const uint8_t*>(base), off, len, init, out,
+                           static_cast<uint64_t>(n),
+                           (mask ? lk::kFlagMask : 0u) | (ps_only ? lk::kFlagPsOnly : 0u),
+                           ctx->d_image, hidx->d_ps + lk::kPsMetaWords, hidx->d_ps, hidx->C, 1u,
+                           fault);
+        rc = LaunchedLp(st, fault);
+        if (rc) return rc;
+        continue;
+      }
       // the stream's pre-pass scratch (none: past kPsStreams streams or out
       // of memory -- the batch takes the default path)
       // (hipStreamPerThread is another queue on every host thread: a scratch
@@ -666,8 +711,7 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         // range into C equal byte chunks (first[c]); the packed kernel then
         // streams it (crc32c_ps.h), or runs the default pipeline when the
         // pre-pass found the batch not packed
-        // (tests, A/Bs: the stream-tiled pipeline even where run_ea suits the batch)
-        static const bool ps_only = getenv("WIPDB_PS_ONLY") && atoi(getenv("WIPDB_PS_ONLY")) != 0;
+        // (tests, A/Bs, ps_only: the stream-tiled pipeline even where run_ea suits the batch)
         const uint32_t C = static_cast<uint32_t>(chunks_per_group * grid);
         std::lock_guard<std::mutex> psl(ps->mu);
         if (++ps->epoch >= (1u << 28)) {  // (the tag's range: start over from a cleared word)
@@ -691,6 +735,7 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                                   hipMemcpyDeviceToHost, st));
         HCRC_CHECK(hipStreamSynchronize(st));
         g_test_ps_meta[0] = (g_test_ps_meta[0] >> 4) == ps->epoch ? (g_test_ps_meta[0] & 15u) : ~0u;
+        g_test_ps_meta[7] = 0u;
 #endif
         hipLaunchKernelGGL(init ? lk::crc32c_lds_packed_kernel<1> : lk::crc32c_lds_packed_kernel<0>,
                            dim3(grid), dim3(lk::kThreads), lk::kLdsBytes, st,
@@ -736,6 +781,108 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
     if (rc) return rc;
   }
   return HCRC_OK;
+}
+
+// HCRC_PACKED's pre-pass restated for a piece the host holds
+// (crc32c_ps.h ps_index: the same promise, the same chunk index): spans
+// sorted, not overlapping, gaps < 4 KiB, no 63 starts within 4 KiB, no
+// position of a chunk past 2^32 from its first page, and not WAL-like (a run
+// of 8 spans under the stream minimum, or 32 of them, among an aligned group
+// of 64).  Writes meta words [0] = 1 << 4 (epoch 1; | kPsBad* bits when the
+// promise is broken), [1..2] chunk bytes, [3..4] the first span's offset, and
+// first[0 .. C] after them.  Returns the kPsBad* bits (0: packed).  On the
+// host a piece costs O(n) over descriptors it already touched -- no pre-pass
+// launch and no floor.
+uint32_t HostPsIndex(const uint64_t* off, const uint32_t* len, size_t n, uint32_t C, uint32_t* ps) {
+  uint32_t* meta = ps;
+  uint32_t* first = ps + lk::kPsMetaWords;
+  for (uint32_t k = 0; k < lk::kPsMetaWords; ++k) meta[k] = 0;
+  if (n == 0 || C == 0) return lk::kPsBad;
+  const uint64_t lo = off[0], hi = off[n - 1] + len[n - 1];
+  const uint64_t range = hi > lo ? hi - lo : 1u;
+  uint64_t cb = (range + C - 1u) / C;
+  cb = (cb + 4095u) & ~uint64_t(4095);
+  if (cb < 4096u) cb = 4096u;
+  uint32_t bad = (cb >> 44) ? lk::kPsBad : 0u;
+  auto chunk_of = [lo, cb, C](uint64_t a) -> uint64_t {
+    if (a < lo) return 0u;
+    const uint64_t c = (a - lo) / cb;
+    return c < C ? c : uint64_t(C);
+  };
+  first[0] = 0;
+  uint64_t prev_c = 0;
+  uint64_t shorts = 0;  // bit j: span 64 g + j of the group is short
+  for (size_t i = 0; i < n && bad == 0u; ++i) {
+    const uint64_t a = off[i];
+    uint64_t c = chunk_of(a);
+    if (a < lo || c >= C) {
+      bad |= lk::kPsBad;
+      break;
+    }
+    if (i > 0) {
+      const uint64_t bp = off[i - 1] + len[i - 1];
+      if (a < bp || a - bp >= 4096u) bad |= lk::kPsBad;
+    }
+    for (uint64_t k = prev_c + 1u; k <= c && i > 0; ++k) first[k] = static_cast<uint32_t>(i);
+    prev_c = c;
+    if (cb + len[i] + 8192u >= (uint64_t(1) << 32)) bad |= lk::kPsBad;
+    if (i + 62 < n) {
+      if (off[i + 62] < a) bad |= lk::kPsBad;
+      else if (off[i + 62] - a < 4096u) bad |= lk::kPsBadDense;
+    }
+    if (len[i] < 96u) shorts |= uint64_t(1) << (i & 63u);
+    if ((i & 63u) == 63u || i + 1 == n) {
+      uint64_t m = shorts;
+      if (__builtin_popcountll(m) >= 32) bad |= lk::kPsBadShort;
+      m &= m >> 1;
+      m &= m >> 2;
+      m &= m >> 4;
+      if (m) bad |= lk::kPsBadShort;
+      shorts = 0;
+    }
+  }
+  if (bad == 0u)
+    for (uint64_t k = prev_c + 1u; k <= C; ++k) first[k] = static_cast<uint32_t>(n);
+  meta[0] = (1u << 4) | bad;
+  meta[1] = static_cast<uint32_t>(cb);
+  meta[2] = static_cast<uint32_t>(cb >> 32);
+  meta[3] = static_cast<uint32_t>(lo);
+  meta[4] = static_cast<uint32_t>(lo >> 32);
+  return bad;
+}
+
+// Host pieces of at least this many spans take a host-built index when the
+// promise holds (WIPDB_PS_MIN_SPANS overrides, as for device batches)
+constexpr size_t kHostPackedMinSpans = 4096;
+size_t HostPackedMinSpans() {
+  static const size_t v = [] {
+    const char* e = getenv("WIPDB_PS_MIN_SPANS");
+    return e && *e ? static_cast<size_t>(atol(e)) : kHostPackedMinSpans;
+  }();
+  return v;
+}
+
+// The piece's index into the slot (host copy, then H2D on st) when the piece
+// may take the packed kernel: no size-class / long-span flag, enough spans,
+// and the promise holds.  Returns the index to launch with, or nullptr.
+const HostIndex* SlotHostIndex(hcrc_ctx* ctx, Slot& s, const uint64_t* h_off, const uint32_t* h_len,
+                               size_t n, int flags, hipStream_t st, HostIndex* keep) {
+  if (flags & (HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG | HCRC_BALANCE)) return nullptr;
+  if (n < HostPackedMinSpans() || n <= kAutoLongSpans) return nullptr;
+  const uint32_t C = static_cast<uint32_t>(PsChunksPerGroup() * LdsGrid(ctx, n));
+  if (C > kPsMaxHostChunks) return nullptr;
+  if (HostPsIndex(h_off, h_len, n, C, s.h_ps) != 0u) return nullptr;
+#ifdef WIPDB_HCRC_TEST_HOOKS
+  for (uint32_t k = 0; k < lk::kPsMetaWords; ++k) g_test_ps_meta[k] = s.h_ps[k];
+  g_test_ps_meta[0] = s.h_ps[0] & 15u;
+  g_test_ps_meta[7] = 0x484F5354u;  // ("HOST": the index was built on the host)
+#endif
+  if (hipMemcpyAsync(s.d_ps, s.h_ps, (lk::kPsMetaWords + C + 1) * 4, hipMemcpyHostToDevice, st) !=
+      hipSuccess)
+    return nullptr;
+  keep->d_ps = s.d_ps;
+  keep->C = C;
+  return keep;
 }
 
 // A host piece of at most kAutoLongSpans spans with one of >= kDevLongSpan
@@ -910,10 +1057,12 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
     HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
     if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
+    const int pflags = flags | AutoSplit(host_base, offsets + i, lengths + i, n) |
+                       AutoLongHost(lengths + i, n);
+    HostIndex hi;
     rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
-                     flags | AutoSplit(host_base, offsets + i, lengths + i, n) |
-                         AutoLongHost(lengths + i, n),
-                     st, AutoLong::kNo, lane.FaultWord());
+                     pflags, st, AutoLong::kNo, lane.FaultWord(),
+                     SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, st, &hi));
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
@@ -962,10 +1111,14 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
     HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
     if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
+    // (the staged layout is the slot's own: spans in order, 16-byte-aligned
+    // cursor, gaps < 32 bytes -- packed whatever the caller's layout was)
+    const int pflags = flags | AutoSplit(base, offsets + i, lengths + i, n) |
+                       AutoLongHost(lengths + i, n);
+    HostIndex hi;
     rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
-                     flags | AutoSplit(base, offsets + i, lengths + i, n) |
-                         AutoLongHost(lengths + i, n),
-                     st, AutoLong::kNo, lane.FaultWord());
+                     pflags, st, AutoLong::kNo, lane.FaultWord(),
+                     SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, st, &hi));
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
@@ -1093,6 +1246,17 @@ __attribute__((visibility("default"))) void hcrc_test_force_fault(int on) {
   g_force_fault.store(on ? 1 : 0);
 }
 // The pre-pass words of the last HCRC_PACKED launch (n <= 8 copied).
+// the host-built packed index of a piece (HostPsIndex), for the CPU test
+// that checks it against a restatement of the device pre-pass
+__attribute__((visibility("default"))) uint32_t hcrc_test_host_ps_index(const uint64_t* off,
+                                                                        const uint32_t* len,
+                                                                        size_t n, uint32_t C,
+                                                                        uint32_t* ps) {
+  return HostPsIndex(off, len, n, C, ps);
+}
+__attribute__((visibility("default"))) void hcrc_test_clear_packed_meta() {
+  for (uint32_t k = 0; k < lk::kPsMetaWords; ++k) g_test_ps_meta[k] = 0xFFFFFFFFu;
+}
 __attribute__((visibility("default"))) void hcrc_test_packed_meta(uint32_t* out, int n) {
   for (int i = 0; i < n && i < static_cast<int>(lk::kPsMetaWords); ++i) out[i] = g_test_ps_meta[i];
 }
