@@ -30,8 +30,10 @@
 // LDB_SO; tests/test_table.py), and leveldb's Table::Open + ReadBlock accept
 // them.
 //
-// Apart from the comparator the adapter calls through (a leveldb deployment
-// links leveldb anyway), only inline members of leveldb's headers are used.
+// Link requirement: the adapter calls leveldb::BytewiseComparator() (the
+// default comparator, not inline), so a program using this header links
+// libleveldb -- a leveldb deployment does anyway; otherwise only inline
+// members of leveldb's headers are used.
 // SupportedOptions says whether a leveldb::Options can be served (no
 // compression -- WipDB's benchmarks run without it, kv_bench.cc:984 -- and
 // no filter or the built-in bloom filter); call it first.
@@ -43,6 +45,7 @@
 #include <mutex>
 #include <string>
 #include <string_view>
+#include <type_traits>
 
 #include "leveldb/comparator.h"
 #include "leveldb/env.h"
@@ -98,17 +101,36 @@ class ComparatorFrom : public table::Comparator {
   const Cmp* c_;
 };
 
-// One wrapper per leveldb comparator, for the life of the process
-// (comparators are long-lived: leveldb::BytewiseComparator() is a
-// singleton, a DB's InternalKeyComparator lives as long as the DB).
+// One wrapper per leveldb comparator, kept by address until
+// ReleaseComparator(c) (leveldb::BytewiseComparator() is a singleton; a DB's
+// InternalKeyComparator lives as long as the DB: call ReleaseComparator when
+// the DB closes, or let the caller own the wrapper -- TableOptionsFrom's
+// `owner` argument -- so that no cache entry is made at all).  Keyed by
+// address, not name: two InternalKeyComparators share a name but may wrap
+// different user comparators.
+template <class Cmp>
+inline std::map<const Cmp*, std::unique_ptr<ComparatorFrom<Cmp>>>& WrapperCache(std::mutex** mu) {
+  static std::mutex m;
+  static auto* cache = new std::map<const Cmp*, std::unique_ptr<ComparatorFrom<Cmp>>>;
+  *mu = &m;
+  return *cache;
+}
 template <class Cmp>
 inline const table::Comparator* WrapComparator(const Cmp* c) {
-  static std::mutex mu;
-  static auto* m = new std::map<const Cmp*, std::unique_ptr<ComparatorFrom<Cmp>>>;
-  std::lock_guard<std::mutex> lk(mu);
-  auto& w = (*m)[c];
+  std::mutex* mu;
+  auto& m = WrapperCache<Cmp>(&mu);
+  std::lock_guard<std::mutex> lk(*mu);
+  auto& w = m[c];
   if (!w) w.reset(new ComparatorFrom<Cmp>(c));
   return w.get();
+}
+// Drops c's cached wrapper (its TableOptions must no longer be in use).
+template <class Cmp>
+inline void ReleaseComparator(const Cmp* c) {
+  std::mutex* mu;
+  auto& m = WrapperCache<Cmp>(&mu);
+  std::lock_guard<std::mutex> lk(*mu);
+  m.erase(c);
 }
 
 // Whether wipdb::table can write what leveldb::TableBuilder would for these
@@ -122,9 +144,9 @@ inline const table::Comparator* WrapComparator(const Cmp* c) {
 // Any comparator is served: its own separators shorten the index keys.  A
 // comparator named "leveldb.InternalKeyComparator" means internal keys (the
 // bloom filter hashes the user key, as InternalFilterPolicy does); the second
-// argument is kept for source compatibility and no longer consulted.
+// argument is DEPRECATED: kept for source compatibility and ignored.
 template <class Opts = leveldb::Options>
-inline bool SupportedOptions(const Opts& o, bool /*internal_user_bytewise*/ = false) {
+inline bool SupportedOptions(const Opts& o, bool /*internal_user_bytewise: deprecated*/ = false) {
   if (o.compression != leveldb::kNoCompression) return false;
   if (o.filter_policy && strcmp(o.filter_policy->Name(), "leveldb.BuiltinBloomFilter2") != 0)
     return false;
@@ -135,10 +157,13 @@ inline bool SupportedOptions(const Opts& o, bool /*internal_user_bytewise*/ = fa
 // SupportedOptions accepts).  leveldb::FilterPolicy does not expose its bits
 // per key, so the caller passes what it gave NewBloomFilterPolicy (0 = no
 // filter policy).  A null comparator is leveldb's default,
-// leveldb::BytewiseComparator().
+// leveldb::BytewiseComparator().  owner (nullable): the comparator wrapper
+// is created into *owner, which must outlive the options; without it the
+// wrapper comes from WrapComparator's cache.
 template <class Opts = leveldb::Options>
 inline table::TableOptions TableOptionsFrom(const Opts& o, int bloom_bits, table::CrcMode mode,
-                                            int device = -1) {
+                                            int device = -1,
+                                            std::unique_ptr<table::Comparator>* owner = nullptr) {
   table::TableOptions t;
   t.block_size = o.block_size;
   t.block_restart_interval = o.block_restart_interval;
@@ -148,7 +173,12 @@ inline table::TableOptions TableOptionsFrom(const Opts& o, int bloom_bits, table
   const auto* c = o.comparator ? o.comparator : leveldb::BytewiseComparator();
   if (strcmp(c->Name(), "leveldb.InternalKeyComparator") == 0)
     t = table::InternalKeyTableOptions(t);  // (user-key bloom filter)
-  t.comparator = WrapComparator(c);
+  if (owner) {
+    owner->reset(new ComparatorFrom<std::remove_cv_t<std::remove_pointer_t<decltype(c)>>>(c));
+    t.comparator = owner->get();
+  } else {
+    t.comparator = WrapComparator(c);
+  }
   return t;
 }
 

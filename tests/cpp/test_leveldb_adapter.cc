@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -121,7 +122,11 @@ int main(int argc, char** argv) {
 
   MemFile file;
   wipdb::leveldbcompat::WritableFileSink<MemFile> sink(&file);
-  wipdb::table::TableBuilder tb(wipdb::leveldbcompat::TableOptionsFrom(o, bloom, mode), &sink);
+  // (the comparator wrapper owned by the caller on odd entry counts, from the
+  // adapter's cache on even ones: the same bytes either way)
+  std::unique_ptr<wipdb::table::Comparator> own;
+  wipdb::table::TableBuilder tb(
+      wipdb::leveldbcompat::TableOptionsFrom(o, bloom, mode, -1, (n & 1) ? &own : nullptr), &sink);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t kl = u32();
     std::string k = in.substr(pos, kl);
