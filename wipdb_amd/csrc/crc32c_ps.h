@@ -313,11 +313,12 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
   // Bytes between a cut and the next reset (trailers, short spans, a chunk's
   // front) are never zeroed: what they leave in the registers no segment uses.
   uint32_t a32 = 0, b32 = 0;      // span [a32, b32)
-  u32x4 hc{0, 0, 0, 0};           // its head chunk, rewritten
-  u32x4 tt{0, 0, 0, 0};           // its tail chunk [E16, E16 + 16) from memory
+  uint32_t hb = 0, inj = 0;       // its head chunk's leading bytes before a, the head register
+  u32x4 tt{0, 0, 0, 0};           // its tail chunk [E16, E16 + 16)
   uint32_t in_r = 0, f_r = 0;     // IN and F at its cut
   uint32_t hwin = 0, cwin = 0;    // the pages (relative indices) of its head chunk and its cut
-  uint32_t ha = 0;                // the LDS address of its head chunk in the slot
+  uint32_t twin = ~0u;            // the page its tail chunk is read from in LDS (~0: none)
+  uint32_t ha = 0, ta = 0;        // the LDS addresses of its head and tail chunks in the slot
   uint32_t cs = 0;                // cut stripe
   uint32_t cv = 0;                // tc: the cut after stripe chunk tc - 1 (1..4)
   // the page events of the desk's stream spans in rank order (lane r: the
@@ -417,8 +418,9 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         id = d0 + l;
         const bool stream = v && n >= kPsMinStream;
         sstream = stream;
-        const uint32_t e16 = b32 & ~15u, h16 = a32 & ~15u, hb = a32 - h16;
-        const uint32_t inj = head_register_lane(l, stream ? iv : 0u, hb);
+        const uint32_t e16 = b32 & ~15u, h16 = a32 & ~15u;
+        hb = a32 - h16;
+        inj = head_register_lane(l, stream ? iv : 0u, hb);
         in_r = f_r = 0;
         // the page events: head chunk (a reset), last chunk (a cut)
         const uint32_t lc = e16 - 16u;
@@ -435,11 +437,17 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           cev = fperm(stream ? (lc >> 12) << 12 | cs << 3 | cv : ~0u, rk);
           hev = fperm(stream ? (h16 >> 12) << 12 | ((h16 & 4095u) >> 6) << 3 | (((h16 & 63u) >> 4) + 1u) : ~0u, rk);
         }
-        // head and tail chunks from memory (each in the span's pages)
-        hc = u32x4{0, 0, 0, 0};
-        if (stream) hc = *reinterpret_cast<const u32x4*>(W0 + h16);
+        // head and tail chunks: read from the page in LDS when it lands
+        // (below), not from memory -- a desk's global loads of them were a
+        // round trip on every desk and 128-byte lines beside the page stream
+        // (the packed 512 B bucket read 1.23 x its bytes, profiles/
+        // r06g_traffic.json).  A tail chunk that starts a page belongs to a
+        // span finished before that page lands: that one comes from memory.
+        ta = ps_lds_addr(pp.slot, e16 & 4095u);
+        const bool tail = stream && (b32 & 15u) != 0u;
+        twin = tail && (e16 & 4095u) != 0u ? e16 >> 12 : ~0u;
         tt = u32x4{0, 0, 0, 0};
-        if (stream && (b32 & 15u) != 0u) tt = *reinterpret_cast<const u32x4*>(W0 + e16);
+        if (tail && (e16 & 4095u) == 0u) tt = *reinterpret_cast<const u32x4*>(W0 + e16);
         // spans off the stream: empty ones (crc = init) and short ones,
         // byte by byte from aligned memory words
         const bool small = v && !stream;
@@ -455,13 +463,6 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
           const uint32_t crc = ~r;
           if (small) out32[id] = msk ? mask_crc(crc) : crc;
         }
-        // the head chunk in its stream form: the bytes before a zeroed, the
-        // head register XORed into its first word
-        loads_landed(hc);
-        hc.x = (hb >= 4u ? 0u : hc.x & ~low_bytes(hb)) ^ inj;
-        hc.y = hb >= 8u ? 0u : (hb <= 4u ? hc.y : hc.y & ~low_bytes(hb - 4u));
-        hc.z = hb >= 12u ? 0u : (hb <= 8u ? hc.z : hc.z & ~low_bytes(hb - 8u));
-        hc.w = hb <= 12u ? hc.w : hc.w & ~low_bytes(hb - 12u);
       }
       // the windows this desk covers: up to the one where its last span
       // starts (the next span may start there)
@@ -506,7 +507,25 @@ __device__ __forceinline__ void run_ps(const Src& src, void* out, uint32_t flags
         // the page has landed: this wave issues ahead of the others' compute
         // until its next DMA is out (as run_lp does)
         if constexpr (kPsPrio != 0) lk_prio<kPsPrio>();
-        if (head) lds_st4(ha, hc);
+        // the tail chunks in this page (as DMA'd: read before any head is
+        // rewritten -- a span's tail chunk may be the next one's head chunk),
+        // then the head chunks in their stream form: the bytes before a
+        // zeroed, the head register XORed into its first word
+        const bool tl = twin == wi;
+        if (ballot(head || tl) != 0u) {
+          u32x4 hc{0, 0, 0, 0}, tv{0, 0, 0, 0};
+          if (head) hc = lds_ld4(ha);
+          if (tl) tv = lds_ld4(ta);
+          lgkm_wait();
+          if (tl) tt = tv;
+          if (head) {
+            hc.x = (hb >= 4u ? 0u : hc.x & ~low_bytes(hb)) ^ inj;
+            hc.y = hb >= 8u ? 0u : (hb <= 4u ? hc.y : hc.y & ~low_bytes(hb - 4u));
+            hc.z = hb >= 12u ? 0u : (hb <= 8u ? hc.z : hc.z & ~low_bytes(hb - 8u));
+            hc.w = hb <= 12u ? hc.w : hc.w & ~low_bytes(hb - 12u);
+            lds_st4(ha, hc);
+          }
+        }
         lds_order();  // the head chunks, then the lanes' reads of the page
         uint32_t W[16];
         pp.read(W);
