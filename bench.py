@@ -230,10 +230,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # WIPDB_BENCH_REHEARSAL=1 (tests only): more ranks than GPUs share the
+    # visible ones and talk over gloo -- rehearses the N > 1 path on a one-GPU
+    # box (RCCL refuses two ranks on one device); the driver's runs are one
+    # rank per GPU over RCCL
+    rehearsal = os.environ.get("WIPDB_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     blocks = a.blocks or ((1 << 20) if world == 1 else (8 << 20))
