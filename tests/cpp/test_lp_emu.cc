@@ -350,11 +350,11 @@ void RunPacked(const char* name, const uint8_t* data0, size_t data_n, const std:
     if (inits)
       crc32c_lds_packed_kernel<1>(data, offs.data(), lens.data(), inits->data(), got.data(), n,
                                   (mask ? kFlagMask : 0u) | g_packed_flags, img, first.data(), meta.data(), C,
-                                  kEpoch, &g_fault_word);
+                                  kEpoch, &g_fault_word, nullptr);
     else
       crc32c_lds_packed_kernel<0>(data, offs.data(), lens.data(), nullptr, got.data(), n,
                                   (mask ? kFlagMask : 0u) | g_packed_flags, img, first.data(), meta.data(), C,
-                                  kEpoch, &g_fault_word);
+                                  kEpoch, &g_fault_word, nullptr);
   });
   char label[96];
   const int pipes = emu::g_pipes.load();

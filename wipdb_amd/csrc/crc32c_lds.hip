@@ -1078,8 +1078,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_packed_kernel(
     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ inits,
     uint32_t* __restrict__ out, uint64_t count, uint32_t flags, const uint8_t* __restrict__ image,
     const uint32_t* __restrict__ first, const uint32_t* __restrict__ meta, uint32_t C,
-    uint32_t epoch, unsigned int* fault) {
+    uint32_t epoch, unsigned int* fault, unsigned int* hint) {
   const DescSrc<INIT != 0> src{base, offsets, lengths, inits, count, 0u, nullptr};
+  // the pre-pass's verdict back to the host (hcrc_api.cc PsScratch::h_hint:
+  // a repeated batch that suits run_ea or is not packed skips the pass next
+  // time); a plain system-scope store, as the fault words
+  if (hint != nullptr && group_id() == 0u && lane_tid() == 0u) {
+#if !defined(WIPDB_LK_EMU)
+    __hip_atomic_store(hint, meta[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+    *hint = meta[0];
+#endif
+  }
   if ((flags & kFlagPsOnly) == 0u && pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
   else if (meta[0] != epoch << 4) run_lp<0>(src, out, flags & kFlagMask, image, fault);
   else run_ps(src, out, flags, image, first, C, fault);
@@ -1088,12 +1098,12 @@ template __global__ void crc32c_lds_packed_kernel<0>(const uint8_t*, const uint6
                                                      const uint32_t*, const uint32_t*, uint32_t*,
                                                      uint64_t, uint32_t, const uint8_t*,
                                                      const uint32_t*, const uint32_t*, uint32_t,
-                                                     uint32_t, unsigned int*);
+                                                     uint32_t, unsigned int*, unsigned int*);
 template __global__ void crc32c_lds_packed_kernel<1>(const uint8_t*, const uint64_t*,
                                                      const uint32_t*, const uint32_t*, uint32_t*,
                                                      uint64_t, uint32_t, const uint8_t*,
                                                      const uint32_t*, const uint32_t*, uint32_t,
-                                                     uint32_t, unsigned int*);
+                                                     uint32_t, unsigned int*, unsigned int*);
 
 // The packed batch's pre-pass (crc32c_ps.h ps_index); epoch: the launch's
 // tag of the verdict word (1 .. 2^28 - 1, the host's per-stream count).

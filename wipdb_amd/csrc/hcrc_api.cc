@@ -48,7 +48,7 @@ template <int INIT>
 __global__ void crc32c_lds_packed_kernel(const uint8_t*, const uint64_t*, const uint32_t*,
                                          const uint32_t*, uint32_t*, uint64_t, uint32_t,
                                          const uint8_t*, const uint32_t*, const uint32_t*, uint32_t,
-                                         uint32_t, unsigned int*);
+                                         uint32_t, unsigned int*, unsigned int*);
 __global__ void crc32c_ps_index_kernel(const uint8_t*, const uint64_t*, const uint32_t*, uint64_t,
                                        uint32_t, uint32_t*, uint32_t*, uint32_t, uint32_t);
 __global__ void crc32c_dma_ceiling_kernel(const uint8_t*, uint64_t, uint32_t*, uint64_t,
@@ -310,6 +310,22 @@ struct hcrc_ctx {
     uint32_t* d = nullptr;
     uint32_t epoch = 0;
     std::mutex mu;  // a launch pair (pre-pass, kernel) is enqueued whole
+    // The verdict of the stream's last pre-pass, as its packed kernel left it
+    // (a pinned word the kernel stores with system scope: epoch << 4 | the
+    // kPsBad* / kPsEa bits), and the batch it was for: the next launch of
+    // the SAME batch (base, columns, count) whose verdict came back "suits
+    // run_ea" or "not packed" skips the pre-pass and runs the spans kernel,
+    // which samples and chooses by itself -- so a repeated batch pays the
+    // pre-pass once, and a wrong hint (the caller rewrote the columns in
+    // place) costs speed, never a CRC.  Re-checked every kHintRecheck skips.
+    uint32_t* h_hint = nullptr;  // pinned, coherent
+    uint32_t* d_hint = nullptr;  // its device view
+    const void* key_base = nullptr;
+    const void* key_off = nullptr;
+    const void* key_len = nullptr;
+    size_t key_n = 0;
+    uint32_t key_epoch = 0;
+    uint32_t skips = 0;
   };
   std::mutex ps_mu;
   std::map<hipStream_t, std::unique_ptr<PsScratch>> ps_scratch;
@@ -547,6 +563,10 @@ constexpr size_t kPackedMinSpans = size_t(1) << 15;
 // streams with a packed scratch of their own (~16 KiB each); further streams'
 // packed batches take the default path
 constexpr size_t kPsStreams = 1024;
+// a repeated batch skips the pre-pass on its last verdict at most this many
+// times in a row, then is checked again (a buffer freed and reallocated at
+// the same address with new contents is re-judged)
+constexpr uint32_t kHintRecheck = 64;
 enum class AutoLong { kNo, kDevice };
 
 #ifdef WIPDB_HCRC_TEST_HOOKS
@@ -614,11 +634,20 @@ hcrc_ctx::PsScratch* PsScratchFor(hcrc_ctx* ctx, hipStream_t st, size_t words) {
   if (it != ctx->ps_scratch.end()) return it->second.get();
   if (ctx->ps_scratch.size() >= kPsStreams) return nullptr;
   auto ps = std::make_unique<hcrc_ctx::PsScratch>();
-  if (hipMalloc(reinterpret_cast<void**>(&ps->d), words * 4) != hipSuccess) return nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&ps->h_hint), 4,
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return nullptr;
+  *ps->h_hint = 0;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&ps->d_hint), ps->h_hint, 0) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&ps->d), words * 4) != hipSuccess) {
+    (void)hipHostFree(ps->h_hint);
+    return nullptr;
+  }
   // the verdict words only, ordered on the caller's stream ahead of its first
   // pre-pass (first[] is written by every pre-pass before it is read)
   if (hipMemsetAsync(ps->d, 0, lk::kPsMetaWords * 4, st) != hipSuccess) {
     (void)hipFree(ps->d);
+    (void)hipHostFree(ps->h_hint);
     return nullptr;
   }
   hcrc_ctx::PsScratch* raw = ps.get();
@@ -692,7 +721,7 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                            static_cast<uint64_t>(n),
                            (mask ? lk::kFlagMask : 0u) | (ps_only ? lk::kFlagPsOnly : 0u),
                            ctx->d_image, hidx->d_ps + lk::kPsMetaWords, hidx->d_ps, hidx->C, 1u,
-                           fault);
+                           fault, static_cast<unsigned int*>(nullptr));
         rc = LaunchedLp(st, fault);
         if (rc) return rc;
         continue;
@@ -702,10 +731,39 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
       // (hipStreamPerThread is another queue on every host thread: a scratch
       // keyed by it would be shared between queues, so its batches take the
       // default path -- ADVICE r5)
-      hcrc_ctx::PsScratch* const ps =
-          (flags & HCRC_PACKED) && n >= packed_min && st != hipStreamPerThread
+      // Device batches of >= packed_min spans take the packed sequence --
+      // flagged (HCRC_PACKED) or not: the pre-pass checks the promise, and a
+      // batch that breaks it, or suits run_ea, runs the default pipelines
+      // inside the packed kernel.  A repeated batch whose last verdict was
+      // one of those skips the pre-pass (PsScratch::h_hint) and runs the
+      // spans kernel below.
+      // (no flag: launches of >= auto_min spans; WIPDB_PS_AUTO_MIN_SPANS for
+      // tests and A/Bs, 0 = never)
+      static const size_t auto_min = [] {
+        const char* e = getenv("WIPDB_PS_AUTO_MIN_SPANS");
+        return e && *e ? static_cast<size_t>(atol(e)) : kPackedMinSpans;
+      }();
+      const bool want_ps =
+          (flags & HCRC_PACKED) ? n >= packed_min
+                                : auto_long == AutoLong::kDevice && (flags & HCRC_BALANCE) == 0 &&
+                                      auto_min != 0 && n >= auto_min;
+      hcrc_ctx::PsScratch* ps =
+          want_ps && st != hipStreamPerThread
               ? PsScratchFor(ctx, st, size_t(chunks_per_group) * ctx->num_cu + 1 + lk::kPsMetaWords)
               : nullptr;
+      std::unique_lock<std::mutex> psl;
+      if (ps) {
+        psl = std::unique_lock<std::mutex>(ps->mu);
+        const bool same = ps->key_base == base && ps->key_off == off + pos &&
+                          ps->key_len == len + pos && ps->key_n == n;
+        const uint32_t h = __atomic_load_n(ps->h_hint, __ATOMIC_ACQUIRE);
+        if (same && (h >> 4) == ps->key_epoch && (h & 15u) != 0u && !ps_only &&
+            ps->skips < kHintRecheck) {
+          ++ps->skips;  // (the last verdict of this batch: run_ea or not packed)
+          ps = nullptr;
+          psl.unlock();
+        }
+      }
       if (ps) {
         // HCRC_PACKED: the pre-pass checks the batch and cuts its covering
         // range into C equal byte chunks (first[c]); the packed kernel then
@@ -713,11 +771,16 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
         // pre-pass found the batch not packed
         // (tests, A/Bs, ps_only: the stream-tiled pipeline even where run_ea suits the batch)
         const uint32_t C = static_cast<uint32_t>(chunks_per_group * grid);
-        std::lock_guard<std::mutex> psl(ps->mu);
         if (++ps->epoch >= (1u << 28)) {  // (the tag's range: start over from a cleared word)
           HCRC_CHECK(hipMemsetAsync(ps->d, 0, lk::kPsMetaWords * 4, st));
           ps->epoch = 1;
         }
+        ps->key_base = base;
+        ps->key_off = off + pos;
+        ps->key_len = len + pos;
+        ps->key_n = n;
+        ps->key_epoch = ps->epoch;
+        ps->skips = 0;
         uint32_t* meta = ps->d;
         uint32_t* first = meta + lk::kPsMetaWords;
         const int pgrid = static_cast<int>(std::max<size_t>(
@@ -743,7 +806,8 @@ int LaunchSpans(hcrc_ctx* ctx, const void* base, const uint64_t* off, const uint
                            init ? init + pos : nullptr, out + pos, static_cast<uint64_t>(n),
                            (mask ? lk::kFlagMask : 0u) |
                                (ps_only ? lk::kFlagPsOnly : 0u),
-                           ctx->d_image, first, meta, C, ps->epoch, fault);
+                           ctx->d_image, first, meta, C, ps->epoch, fault,
+                           reinterpret_cast<unsigned int*>(ps->d_hint));
         rc = LaunchedLp(st, fault);
         if (rc) return rc;
         continue;
@@ -1377,8 +1441,10 @@ hcrc_ctx::~hcrc_ctx() {
     (void)hipMemPoolDestroy(scratch_pool);
   }
   if (fault_words) (void)hipHostFree(fault_words);
-  for (auto& kv : ps_scratch)
+  for (auto& kv : ps_scratch) {
     if (kv.second->d) (void)hipFree(kv.second->d);
+    if (kv.second->h_hint) (void)hipHostFree(kv.second->h_hint);
+  }
 }
 
 void* hcrc_ctx_stream(hcrc_ctx* ctx) { return ctx ? ctx->stream : nullptr; }
@@ -1616,6 +1682,7 @@ int hcrc_stream_forget(hcrc_ctx* ctx, void* stream) {
     // (the caller's launches on the stream are complete; hipFree waits for
     // the device anyway)
     if (hipFree(ps->d) != hipSuccess) return HCRC_ERR_HIP;
+    if (ps->h_hint && hipHostFree(ps->h_hint) != hipSuccess) return HCRC_ERR_HIP;
   }
   return any ? HCRC_ERR_KERNEL : HCRC_OK;
 }
