@@ -57,8 +57,9 @@ Also printed in the same JSON line:
                 K / 2 (frac_of_ceiling_alternating; the same power and
                 clock state for both).  roofline.timed_dispatch_first
                 = the index of the first timed launch among this process's
-                spans-kernel dispatches (scripts/trace_timed.py picks the K
-                timed ones out of a rocprofv3 kernel trace).
+                CRC-kernel dispatches (spans or packed kernel, one a
+                step; scripts/trace_timed.py picks the K timed ones out of
+                a rocprofv3 kernel trace).
   config3_mixed, table_blocks, verified_table_blocks, config5_pcie
                 (rank 0, N = 1, after the headline; --no-extra skips them)
                 BASELINE configs[2] and [4] under the same clock: config 3's
