@@ -112,23 +112,30 @@ extern "C" {
  * the passes would only add two launches per staged piece). */
 #define HCRC_BALANCE 0x10
 /* SST-packed device batch (hcrc_batch_async / hcrc_batch with
- * HCRC_DEVICE_PTRS): the caller says the spans are sorted by offset, do not
- * overlap and leave gaps of less than 4 KiB -- what TableBuilder::
- * WriteRawBlock leaves in a write buffer (kv/src/table/table_builder.cc:
- * 183-202), a WAL block, config 3's stream.  The batch is then read as ONE
- * byte stream, 4 KiB page by page, fully coalesced, each workgroup an equal
- * share of the bytes (stream-tiled kernel).  A small
- * pre-pass checks the promise (and that no 4 KiB holds more than 62 span
- * starts); a batch that breaks it runs the default pipeline instead, so
- * the flag can cost speed, never a CRC; a batch the default pipeline's
- * end-aligned loop suits (aligned 4 KiB blocks, table blocks, spans of >= 16
- * KiB) runs that loop.  Scratch: (16 G + 9) * 4 bytes per stream that
- * launches one, allocated on its first and kept with the context.
- * Ignored with HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG; HCRC_BALANCE is implied.
- * On host pointers it applies to the device-side layout of each piece
- * (staged pieces are packed by construction).  A launch of fewer than 32 Ki
- * spans runs the default path: the pre-pass costs ~10 us a call, which the
- * stream repays only on batches of more than ~128 MiB of short spans. */
+ * HCRC_DEVICE_PTRS): the spans are sorted by offset, do not overlap and
+ * leave gaps of less than 4 KiB -- what TableBuilder::WriteRawBlock leaves
+ * in a write buffer (kv/src/table/table_builder.cc:183-202), a WAL block,
+ * config 3's stream.  Such a batch is read as ONE byte stream, 4 KiB page by
+ * page, fully coalesced, each workgroup an equal share of the bytes
+ * (stream-tiled kernel).  A small pre-pass checks the
+ * promise (and that no 4 KiB holds more than 62 span starts); a batch that
+ * breaks it runs the default pipelines instead, and one the end-aligned
+ * loop suits (aligned 4 KiB blocks, table blocks, spans of >= 16 KiB) runs
+ * that loop, so the promise can cost speed, never a CRC.
+ *   Since round 6 no flag is needed: every device batch of >= 32 Ki spans
+ * takes this sequence, and a REPEATED batch (same base, columns and count on
+ * the same stream) whose last verdict was "suits the end-aligned loop" or
+ * "not packed" skips the pre-pass (the verdict comes back through a pinned
+ * word the kernel stores; re-checked every 64 launches).  The flag lowers
+ * the minimum (WIPDB_PS_MIN_SPANS, tests) and keeps HCRC_BALANCE batches on
+ * this path.  Host batches build the check and the chunk index on the host
+ * for every piece of >= 4096 spans (staged pieces are packed by
+ * construction).  Scratch: (16 G + 9) * 4 bytes and a pinned word per
+ * stream that launches one, allocated on its first and kept with the
+ * context (hcrc_stream_forget releases them).  Ignored with
+ * HCRC_SPLIT_SMALL / HCRC_SPLIT_LONG.  Below 32 Ki spans the default kernel
+ * runs: there the stream's start (desk loads, a page a wave) is slower than
+ * the default kernel (one 2 MiB SST of 488 spans: 15 vs 24 us). */
 #define HCRC_PACKED 0x20
 
 typedef struct hcrc_ctx hcrc_ctx;
