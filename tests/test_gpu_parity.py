@@ -1826,55 +1826,55 @@ def test_default_device_batches_take_the_packed_sequence():
     CRC against the oracle."""
     assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
     code = (
-        "import ctypes, json, sys, numpy as np, torch\\n"
-        "sys.path.insert(0, 'tests')\\n"
-        "from conftest import Oracle\\n"
-        "from wipdb_amd import Engine, _lib\\n"
-        "lib = _lib.load()\\n"
-        "ora = Oracle()\\n"
-        "rng = np.random.default_rng(31)\\n"
-        "def lay(n, lo, hi, g, start=3):\\n"
-        "    l = rng.integers(lo, hi + 1, n).astype(np.uint64)\\n"
-        "    return start + np.concatenate([[0], np.cumsum(l + g)[:-1]]).astype(np.uint64), l.astype(np.uint32)\\n"
-        "n = 40000\\n"
-        "cases = {'short': lay(n, 512, 2200, 5), 'a4k': (np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096, np.uint32))}\\n"
-        "o, l = lay(n, 300, 3000, 5)\\n"
-        "o[[10, 11]] = o[[11, 10]]\\n"
-        "cases['unsorted'] = (o, l)\\n"
-        "size = max(int((o + l).max()) for o, l in cases.values()) + 64\\n"
-        "host = rng.integers(0, 256, size, dtype=np.uint8)\\n"
-        "res, bad = {}, []\\n"
-        "def meta():\\n"
-        "    m = (ctypes.c_uint32 * 8)()\\n"
-        "    lib.hcrc_test_packed_meta(m, 8)\\n"
-        "    return int(m[0])\\n"
-        "with Engine(0) as eng:\\n"
-        "    d = torch.from_numpy(host).cuda()\\n"
-        "    for k, (o, l) in cases.items():\\n"
-        "        do = torch.from_numpy(o.view(np.int64)).cuda()\\n"
-        "        dl = torch.from_numpy(l.view(np.int32)).cuda()\\n"
-        "        want = ora.batch(host, o, l)\\n"
-        "        seen = []\\n"
-        "        for rep in range(3):\\n"
-        "            lib.hcrc_test_clear_packed_meta()\\n"
-        "            out = eng.batch_device(d, do, dl)\\n"
-        "            torch.cuda.synchronize()\\n"
-        "            seen.append(meta())\\n"
-        "            if not (out.cpu().numpy().view(np.uint32) == want).all():\\n"
-        "                bad.append((k, rep))\\n"
-        "        res[k] = seen\\n"
-        "        if k == 'a4k':  # the columns rewritten in place: a packed short-span layout\\n"
-        "            o2, l2 = cases['short']\\n"
-        "            do.copy_(torch.from_numpy(o2.view(np.int64)))\\n"
-        "            dl.copy_(torch.from_numpy(l2.view(np.int32)))\\n"
-        "            lib.hcrc_test_clear_packed_meta()\\n"
-        "            out = eng.batch_device(d, do, dl)\\n"
-        "            torch.cuda.synchronize()\\n"
-        "            res['rewritten'] = [meta()]\\n"
-        "            if not (out.cpu().numpy().view(np.uint32) == ora.batch(host, o2, l2)).all():\\n"
-        "                bad.append(('rewritten', 0))\\n"
-        "print('META ' + json.dumps(res))\\n"
-        "print('BAD', bad)\\n")
+        "import ctypes, json, sys, numpy as np, torch\n"
+        "sys.path.insert(0, 'tests')\n"
+        "from conftest import Oracle\n"
+        "from wipdb_amd import Engine, _lib\n"
+        "lib = _lib.load()\n"
+        "ora = Oracle()\n"
+        "rng = np.random.default_rng(31)\n"
+        "def lay(n, lo, hi, g, start=3):\n"
+        "    l = rng.integers(lo, hi + 1, n).astype(np.uint64)\n"
+        "    return start + np.concatenate([[0], np.cumsum(l + g)[:-1]]).astype(np.uint64), l.astype(np.uint32)\n"
+        "n = 40000\n"
+        "cases = {'short': lay(n, 512, 2200, 5), 'a4k': (np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096, np.uint32))}\n"
+        "o, l = lay(n, 300, 3000, 5)\n"
+        "o[[10, 11]] = o[[11, 10]]\n"
+        "cases['unsorted'] = (o, l)\n"
+        "size = max(int((o + l).max()) for o, l in cases.values()) + 64\n"
+        "host = rng.integers(0, 256, size, dtype=np.uint8)\n"
+        "res, bad = {}, []\n"
+        "def meta():\n"
+        "    m = (ctypes.c_uint32 * 8)()\n"
+        "    lib.hcrc_test_packed_meta(m, 8)\n"
+        "    return int(m[0])\n"
+        "with Engine(0) as eng:\n"
+        "    d = torch.from_numpy(host).cuda()\n"
+        "    for k, (o, l) in cases.items():\n"
+        "        do = torch.from_numpy(o.view(np.int64)).cuda()\n"
+        "        dl = torch.from_numpy(l.view(np.int32)).cuda()\n"
+        "        want = ora.batch(host, o, l)\n"
+        "        seen = []\n"
+        "        for rep in range(3):\n"
+        "            lib.hcrc_test_clear_packed_meta()\n"
+        "            out = eng.batch_device(d, do, dl)\n"
+        "            torch.cuda.synchronize()\n"
+        "            seen.append(meta())\n"
+        "            if not (out.cpu().numpy().view(np.uint32) == want).all():\n"
+        "                bad.append((k, rep))\n"
+        "        res[k] = seen\n"
+        "        if k == 'a4k':  # the columns rewritten in place: a packed short-span layout\n"
+        "            o2, l2 = cases['short']\n"
+        "            do.copy_(torch.from_numpy(o2.view(np.int64)))\n"
+        "            dl.copy_(torch.from_numpy(l2.view(np.int32)))\n"
+        "            lib.hcrc_test_clear_packed_meta()\n"
+        "            out = eng.batch_device(d, do, dl)\n"
+        "            torch.cuda.synchronize()\n"
+        "            res['rewritten'] = [meta()]\n"
+        "            if not (out.cpu().numpy().view(np.uint32) == ora.batch(host, o2, l2)).all():\n"
+        "                bad.append(('rewritten', 0))\n"
+        "print('META ' + json.dumps(res))\n"
+        "print('BAD', bad)\n")
     env = dict(os.environ, PYTHONPATH=REPO, WIPDB_HCRC_LIB=TEST_LIB)
     env.pop("WIPDB_HCRC_FORCE_FAULT", None)
     env.pop("WIPDB_PS_AUTO_MIN_SPANS", None)
