@@ -1025,7 +1025,12 @@ namespace lk {
 // LDS aux column differently) and a mixed batch stays on run_lp.  The choice
 // changes speed only: both compute every span exactly.
 // ---------------------------------------------------------------------------
-template <bool kV, typename Src>
+// kLong: the chunks from which a span counts as long (16 KiB; the packed
+// kernel and its pre-pass: 32 KiB -- spans of 16..32 KiB run faster
+// streamed, 5941-5947 vs 5535-5558 GiB/s on config 3's 16 KiB bucket, while
+// 32 KiB ones do not, 5835-5844 vs 5977-5985, same session,
+// profiles/r06q_pick_ab.log)
+template <bool kV, uint32_t kLong = 4u * kSegChunks, typename Src>
 __device__ __forceinline__ bool pick_ea(const Src& src) {
   const uint32_t l = lane_tid() & 63u;
   const uint64_t count = src.count;
@@ -1037,7 +1042,7 @@ __device__ __forceinline__ bool pick_ea(const Src& src) {
                           src.bytes(n), kV);
   // one segment + a front of <= 16 chunks (run_ea's batched pieces), or a
   // span of >= 16 KiB
-  const bool ok = p.empty || (p.C >= kSegChunks && p.C <= kSegChunks + 16u) || p.C >= 4u * kSegChunks;
+  const bool ok = p.empty || (p.C >= kSegChunks && p.C <= kSegChunks + 16u) || p.C >= kLong;
   return pipeline_marker(ballot(!ok) == 0u);
 }
 
@@ -1065,6 +1070,9 @@ template __global__ void crc32c_lds_spans_kernel<1>(const uint8_t*, const uint64
                                                     uint64_t, uint32_t, const uint8_t*,
                                                     const uint32_t*, unsigned int*);
 
+// the packed kernel's (and its pre-pass's) long-span bound for run_ea
+constexpr uint32_t kPsLongChunks = 8u * kSegChunks;
+
 // Packed batch (HCRC_PACKED, crc32c_ps.h): run_ea when the batch suits it
 // (pick_ea: aligned 4 KiB blocks, table blocks, spans of >= 16 KiB -- where it
 // is 4-7 % faster than run_ps, profiles/r05v_ab.log), else run_ps when the
@@ -1090,7 +1098,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_lds_packed_kernel(
     *hint = meta[0];
 #endif
   }
-  if ((flags & kFlagPsOnly) == 0u && pick_ea<false>(src)) run_ea<0>(src, out, flags & kFlagMask, image);
+  if ((flags & kFlagPsOnly) == 0u && pick_ea<false, kPsLongChunks>(src))
+    run_ea<0>(src, out, flags & kFlagMask, image);
   else if (meta[0] != epoch << 4) run_lp<0>(src, out, flags & kFlagMask, image, fault);
   else run_ps(src, out, flags, image, first, C, fault);
 }
@@ -1119,7 +1128,7 @@ __global__ __launch_bounds__(kPsIndexThreads) void crc32c_ps_index_kernel(
     uint32_t* __restrict__ meta, uint32_t epoch, uint32_t flags) {
   if ((flags & kFlagPsOnly) == 0u) {
     const DescSrc<false> src{base, offsets, lengths, nullptr, count, 0u, nullptr};
-    if (pick_ea<false>(src)) {
+    if (pick_ea<false, kPsLongChunks>(src)) {
       if (group_id() == 0u && lane_tid() == 0u) global_max(meta, (epoch << 4) | kPsEa);
       return;
     }
