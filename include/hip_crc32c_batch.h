@@ -267,10 +267,16 @@ int hcrc_batch_multi_ex(const int* devices, int ndev, const void* base,
 /* Pinned host memory.  hcrc_batch over spans that each lie inside a range
  * allocated by hcrc_host_alloc or registered by hcrc_host_register (e.g.
  * mmap'd SST files, a long-lived memtable arena, a table builder's write
- * buffers -- one or several ranges) runs zero-copy: the kernel reads the
- * spans over PCIe directly, with no staging copy.  Anything else (a span in
- * pageable memory, memory pinned by other means, a span straddling two
- * ranges) sends the batch through the pinned staging slots. */
+ * buffers -- one or several ranges) needs no staging copy: a dense,
+ * in-order piece of >= 8 MiB inside one range (up to 128 MiB a piece; the
+ * last piece of a batch after such a piece has no floor) is copied to the
+ * device by the copy engine, the next piece's copy running under this
+ * one's kernel, and checked out of HBM; any other piece (smaller batches,
+ * sparse or shuffled spans) runs zero-copy: the kernel reads the spans over
+ * PCIe directly.  Anything else (a span in pageable memory, memory pinned by
+ * other means, a span straddling two ranges) sends the batch through the
+ * pinned staging slots.  The copy-engine pieces use two 128 MiB device
+ * buffers per concurrent caller, allocated on first use. */
 int hcrc_host_alloc(size_t bytes, void** out_ptr);
 int hcrc_host_free(void* ptr);
 int hcrc_host_register(void* ptr, size_t bytes);

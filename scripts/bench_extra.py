@@ -384,7 +384,7 @@ def run_sst_pinned(eng, rng, n_sst):
     try:
         host = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(pin.value))
         host[:] = rng.integers(32, 127, nbytes, dtype=np.uint8)
-        eng.batch(host, offs[:1000], lens[:1000])
+        eng.batch(host, offs, lens)  # warm: the slots and the copy-engine buffers allocated
         reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):

@@ -1077,6 +1077,126 @@ def test_host_batches_take_the_host_index():
         assert res[k][1] != host, (k, res)
 
 
+_PINNED_PIECES_CODE = r"""
+import ctypes, json, sys, numpy as np
+sys.path.insert(0, 'tests')
+from conftest import Oracle
+from wipdb_amd import Engine, _lib
+lib = _lib.load()
+ora = Oracle()
+rng = np.random.default_rng(31)
+def lay(n, lo, hi, g, start):
+    l = rng.integers(lo, hi + 1, n).astype(np.uint64)
+    return start + np.concatenate([[0], np.cumsum(l + g)[:-1]]).astype(np.uint64), l.astype(np.uint32)
+size = 300 << 20
+pieces = (ctypes.c_uint64 * 2)()
+res, bad = {}, []
+def run(name, buf, o, l, sample=None):
+    iv = rng.integers(0, 2**32, o.size, dtype=np.uint64).astype(np.uint32)
+    lib.hcrc_test_pinned_pieces(pieces)
+    for inits, m in ((None, False), (iv, True)):
+        got = eng.batch(buf, o, l, inits, mask_output=m)
+        idx = np.arange(o.size) if sample is None else rng.choice(o.size, sample, replace=False)
+        want = ora.batch(np.asarray(buf), o[idx], l[idx], None if inits is None else inits[idx], mask=m)
+        if not (got[idx] == want).all():
+            bad.append((name, m, int((got[idx] != want).sum())))
+    lib.hcrc_test_pinned_pieces(pieces)
+    res[name] = [int(pieces[0]), int(pieces[1])]
+with Engine(0) as eng:
+    pin = ctypes.c_void_p()
+    _lib.check(lib.hcrc_host_alloc(size, ctypes.byref(pin)), 'alloc')
+    buf = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(pin.value))
+    buf[:] = rng.integers(0, 256, size, dtype=np.uint8)
+    # one SST (table blocks + trailers, ~2 MiB): zero-copy, it returns sooner
+    run('sst', buf, *lay(480, 4097, 4225, 4, 7))
+    # 75 MiB of them, a start off the 256-byte grid: one copied piece
+    run('sst75', buf, *lay(18000, 4097, 4225, 4, 7), sample=6000)
+    # 290 MB: three copied pieces (128 MiB each at most)
+    run('sst290', buf, *lay(70000, 4097, 4225, 4, 3), sample=6000)
+    # spans from the very first byte of the range, aligned blocks
+    run('aligned', buf, np.arange(4096, dtype=np.uint64) * 4096, np.full(4096, 4096, np.uint32))
+    # random spans all over the range: not dense, zero-copy
+    l = rng.integers(0, 5000, 3000).astype(np.uint32)
+    o = np.array([int(rng.integers(0, size - int(x))) for x in l], np.uint64)
+    run('sparse', buf, o, l)
+    # an order break after 40 spans: too short a piece, all zero-copy
+    o, l = lay(9000, 300, 3000, 5, 11)
+    o[[40, 41]] = o[[41, 40]]
+    run('unsorted_early', buf, o, l)
+    # an order break after 12 MiB: a copied piece, then the rest
+    o, l = lay(8000, 2000, 4000, 5, 11)
+    k = int(np.searchsorted(o, 12 << 20))
+    o[[k, k + 1]] = o[[k + 1, k]]
+    run('unsorted_late', buf, o, l)
+    # 128 MiB and a 2 MiB tail: the tail is copied behind the first piece
+    run('tail', buf, *lay(32700, 4097, 4225, 4, 5), sample=4000)
+    # 20 MiB in order, then 200 shuffled spans: a copied piece, then zero-copy
+    o, l = lay(5200, 4097, 4225, 4, 9)
+    p = rng.permutation(200)
+    o[-200:], l[-200:] = o[-200:][p], l[-200:][p]
+    run('unsorted_tail', buf, o, l)
+    # the last span ending on the range's last byte
+    o, l = lay(3000, 3000, 5000, 1, 0)
+    o += np.uint64(size - int(o[-1] + l[-1]))
+    run('to_end', buf, o, l)
+    # two registered ranges back to back (one numpy buffer, two registrations)
+    raw = np.empty((40 << 20) + 8192, np.uint8)
+    a0 = (-raw.ctypes.data) % 4096
+    reg = raw[a0:a0 + (40 << 20)]
+    reg[:] = rng.integers(0, 256, reg.size, dtype=np.uint8)
+    half = 20 << 20
+    _lib.check(lib.hcrc_host_register(reg.ctypes.data, half), 'reg1')
+    _lib.check(lib.hcrc_host_register(reg.ctypes.data + half, reg.size - half), 'reg2')
+    o, l = lay(9000, 4000, 4400, 0, 5)
+    keep = ((o + l <= half) | (o >= half)) & (o + l <= reg.size)
+    run('two_ranges', reg, o[keep], l[keep], sample=3000)
+    lib.hcrc_host_unregister(reg.ctypes.data)
+    lib.hcrc_host_unregister(reg.ctypes.data + half)
+    lib.hcrc_host_free(pin)
+print('PIECES ' + json.dumps(res))
+print('BAD', bad)
+"""
+
+
+@pytest.mark.parametrize("dma", ["1", "0"])
+def test_pinned_batches_copy_dense_pieces(dma):
+    """Pinned / registered host batches: a dense, in-order piece of >= 8 MiB
+    is copied to the device by the copy engine and checked out of HBM; a
+    smaller, sparse or shuffled one runs zero-copy (test build: the pieces
+    each way).  One SST, 75 MiB and 290 MB (three 128 MiB pieces) of them,
+    a short tail behind a copied piece, spans from a range's first and to its
+    last byte, order breaks early and late, shuffled spans after a copied
+    piece, two back-to-back registered ranges -- every CRC (a sample on the
+    big ones; inits, masked) against the oracle, with the copy engine on and
+    off (WIPDB_HOST_DMA=0)."""
+    assert os.path.exists(TEST_LIB), "make -C wipdb_amd/csrc builds the test library"
+    env = dict(os.environ, PYTHONPATH=REPO, WIPDB_HCRC_LIB=TEST_LIB, WIPDB_HOST_DMA=dma)
+    env.pop("WIPDB_HCRC_FORCE_FAULT", None)
+    r = subprocess.run([sys.executable, "-c", _PINNED_PIECES_CODE], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "BAD []" in r.stdout, r.stdout[-2000:]
+    import json
+    res = json.loads(r.stdout.split("PIECES ", 1)[1].splitlines()[0])
+    print(res)
+    # (spans over two ranges run zero-copy only when both are identity-mapped,
+    # MappedSpans; otherwise the batch is staged and neither count moves)
+    two = res.pop("two_ranges")
+    if dma == "0":
+        assert all(v[0] == 0 and v[1] > 0 for v in res.values()), res
+        assert two[0] == 0, two
+        return
+    # [copied pieces, zero-copy pieces] over the two calls of each case
+    assert res["sst"] == [0, 2], res
+    for k in ("sst75", "aligned", "to_end"):
+        assert res[k] == [2, 0], (k, res)
+    assert res["sst290"] == [6, 0], res
+    assert res["sparse"] == [0, 2] and res["unsorted_early"] == [0, 2], res
+    assert res["unsorted_late"] == [4, 0] and res["tail"] == [4, 0], res
+    assert res["unsorted_tail"] == [2, 2], res
+    assert two == [0, 0] or two == [4, 0], two
+
+
 def _run_device_packed(engine, buf, offs, lens):
     out = engine.batch_device(_t(buf), _t(np.asarray(offs, np.uint64)),
                               _t(np.asarray(lens, np.uint32)), packed=True)

@@ -150,6 +150,10 @@ struct Slot {
   uint32_t* d_ps = nullptr;
   size_t cap_bytes = 0;
   hipEvent_t done = nullptr;
+  // the copy engine's pieces of pinned batches (BatchZeroCopy): a device
+  // buffer of kDmaBytes and the event of its copy, made on first use
+  uint8_t* d_copy = nullptr;
+  hipEvent_t copied = nullptr;
   // results still to be copied out to the caller once `done` fires
   uint32_t* user_out = nullptr;
   size_t n_out = 0;
@@ -168,6 +172,8 @@ struct Slot {
     if (d_out) (void)hipFree(d_out);
     if (d_ps) (void)hipFree(d_ps);
     if (done) (void)hipEventDestroy(done);
+    if (d_copy) (void)hipFree(d_copy);
+    if (copied) (void)hipEventDestroy(copied);
     *this = Slot();
   }
   // All buffers, or none (a partial failure frees what it got).
@@ -232,6 +238,7 @@ struct Slot {
 // (one piece is copied and computed while the next is packed).
 struct Lane {
   hipStream_t stream = nullptr;
+  hipStream_t copy = nullptr;  // the copy engine's pieces (BatchZeroCopy), made on first use
   Slot slots[2];
   bool slots_ready = false;
   int index = 0;  // 1 .. kMaxLanes: its fault word (hcrc_ctx::fault_words[index])
@@ -279,6 +286,19 @@ const uint8_t* MappedSpans(const uint8_t* base, const uint64_t* offsets, const u
   }
   if (several) return identity ? base : nullptr;
   return hit->second.dev - (hit->first - reinterpret_cast<uintptr_t>(base));
+}
+
+// The pinned or registered range holding host address a: [*lo, *hi), or false.
+bool PinnedRangeOf(uintptr_t a, uintptr_t* lo, uintptr_t* hi) {
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  auto& m = HostRanges();
+  auto it = m.upper_bound(a);
+  if (it == m.begin()) return false;
+  --it;
+  if (a >= it->first + it->second.bytes) return false;
+  *lo = it->first;
+  *hi = it->first + it->second.bytes;
+  return true;
 }
 
 }  // namespace
@@ -370,6 +390,7 @@ class LaneLease {
     for (const Slot& s : lane_->slots) pending = pending || s.user_out != nullptr;
     if (pending) {
       if (lane_->stream) (void)hipStreamSynchronize(lane_->stream);
+      if (lane_->copy) (void)hipStreamSynchronize(lane_->copy);
       for (Slot& s : lane_->slots) {
         s.user_out = nullptr;
         s.n_out = 0;
@@ -578,6 +599,8 @@ std::atomic<int> g_force_fault{-1};
 // the last packed launch's pre-pass words (meta[0]: 0 = streamed, else the
 // kPsBad* bits of the fallback; meta[1..2]: chunk bytes)
 uint32_t g_test_ps_meta[lk::kPsMetaWords];
+// pieces of pinned batches copied by the copy engine / run zero-copy
+std::atomic<uint64_t> g_test_dma_pieces{0}, g_test_zc_pieces{0};
 bool ForcedFault() {
   int f = g_force_fault.load();
   if (f < 0) {
@@ -1099,9 +1122,65 @@ void PackSpans(Slot& s, const uint8_t* base, const uint64_t* offsets, const uint
   else CopyPool::Get().Run(n, copy);
 }
 
-// Zero-copy: the kernel reads the spans straight out of mapped host memory
-// over PCIe (no staging copy, no device buffer); only the descriptors and
-// the results cross through the slots.
+// Whether pinned batches copy their dense pieces with the copy engine
+// (WIPDB_HOST_DMA=0: every piece zero-copy; A/Bs only)
+bool HostDma() {
+  static const bool v = [] {
+    const char* e = getenv("WIPDB_HOST_DMA");
+    return !(e && *e && atoi(e) == 0);
+  }();
+  return v;
+}
+
+// The copy engine's pieces: at most kDmaBytes of covering range (a slot's
+// d_copy), at least kDmaMinBytes -- a smaller batch returns sooner zero-copy
+// (one ~2 MiB SST a call: 73 us p50 zero-copy, 83 us copied); the last
+// piece of a batch after a copied one has no floor
+constexpr size_t kDmaBytes = size_t(128) << 20;
+constexpr size_t kDmaMinBytes = size_t(8) << 20;
+
+// A dense piece of a pinned batch for the copy engine: spans [i, j) in
+// address order inside ONE pinned range whose covering bytes fit cap bytes
+// (at the source address mod 256), hold at most an eighth + 64 KiB more than
+// the spans and at least kDmaMinBytes, unless it ends the batch after a
+// copied piece (tail); [*a, *b) is the range to copy.  Returns j, or i when
+// the piece starting at i is not such a piece (it runs zero-copy).
+size_t DensePiece(const uint8_t* host_base, const uint64_t* offsets, const uint32_t* lengths,
+                  size_t i, size_t count, size_t cap, bool tail, uintptr_t* a, uintptr_t* b) {
+  const uintptr_t first = reinterpret_cast<uintptr_t>(host_base + offsets[i]);
+  uintptr_t rlo, rhi;
+  if (!PinnedRangeOf(first, &rlo, &rhi)) return i;
+  const uintptr_t lim = std::min(rhi, first - (first & 255u) + cap);
+  uintptr_t hi = first, prev = first;
+  uint64_t bytes = 0;
+  size_t j = i;
+  while (j < count && j - i < kStageSpans) {
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(host_base + offsets[j]);
+    const uintptr_t end = lo + lengths[j];
+    if (lo < prev || end > lim) break;
+    prev = lo;
+    hi = std::max(hi, end);
+    bytes += lengths[j];
+    ++j;
+  }
+  if (j == i || hi - first > bytes + bytes / 8 + (uint64_t(64) << 10)) return i;
+  if (hi - first < kDmaMinBytes && !(tail && j == count)) return i;
+  // the copy widened to the 256-byte grid inside the range: the copy engine
+  // runs unaligned host copies at a fraction of its rate
+  *a = std::max(rlo, first & ~uintptr_t(255));
+  *b = std::min(rhi, (hi + 255) & ~uintptr_t(255));
+  return j;
+}
+
+// Pinned batches: a dense piece (DensePiece) is copied into the slot's
+// d_copy by the copy engine -- the PCIe bytes are the covering range once,
+// at the copy engine's rate -- on the lane's copy stream, and the kernel
+// reads it out of HBM on the lane's stream once the copy's event fires, so
+// the next piece's copy runs under this piece's descriptors, kernel and
+// results; any other piece runs zero-copy: the kernel reads the spans
+// straight out of mapped host memory over PCIe (no device buffer; its read
+// windows cross PCIe, so it trails the copy engine on unaligned spans).  The
+// descriptors and the results cross through the slots either way.
 int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
                   const uint8_t* host_base, const uint64_t* offsets, const uint32_t* lengths,
                   const uint32_t* inits, uint32_t* out, size_t count, int flags) {
@@ -1109,13 +1188,46 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
   if (const int frc = lane.FaultsBefore()) return frc;
   size_t i = 0, piece = 0;
   int k = 0;
+  bool copying = false;
   while (i < count) {
     Slot& s = lane->slots[k];
     int rc = s.Drain();
     if (rc) return rc;
     if (InjectedPieceFault(piece++)) return HCRC_ERR_LAUNCH;
-    const size_t n = std::min(count - i, kStageSpans);
-    memcpy(s.h_off, offsets + i, n * 8);
+    // (the last piece after a copied one has no floor: its copy queues
+    // behind that one's)
+    uintptr_t ca = 0, cb = 0;
+    const size_t j =
+        HostDma() ? DensePiece(host_base, offsets, lengths, i, count, kDmaBytes, copying, &ca, &cb)
+                  : i;
+    const bool dma = j > i;
+    copying = dma;
+    const size_t n = dma ? j - i : std::min(count - i, kStageSpans);
+#ifdef WIPDB_HCRC_TEST_HOOKS
+    ++(dma ? g_test_dma_pieces : g_test_zc_pieces);
+#endif
+    const uint8_t* kbase = dev_base;
+    if (dma) {
+      // the covering range at its address mod 256 in the slot
+      const uintptr_t at = ca & 255u;
+      const uintptr_t rebase = ca - at - reinterpret_cast<uintptr_t>(host_base);
+      for (size_t q = 0; q < n; ++q) s.h_off[q] = offsets[i + q] - rebase;
+      if (!lane->copy) HCRC_CHECK(hipStreamCreateWithFlags(&lane->copy, hipStreamNonBlocking));
+      if (!s.d_copy) {
+        if (hipMalloc(reinterpret_cast<void**>(&s.d_copy), kDmaBytes) != hipSuccess) {
+          s.d_copy = nullptr;
+          return HCRC_ERR_NO_MEMORY;
+        }
+        HCRC_CHECK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+      }
+      // (the slot's previous piece is drained: its kernel is done with d_copy)
+      HCRC_CHECK(hipMemcpyAsync(s.d_copy + at, reinterpret_cast<const void*>(ca), cb - ca,
+                                hipMemcpyHostToDevice, lane->copy));
+      HCRC_CHECK(hipEventRecord(s.copied, lane->copy));
+      kbase = s.d_copy;
+    } else {
+      memcpy(s.h_off, offsets + i, n * 8);
+    }
     memcpy(s.h_len, lengths + i, n * 4);
     if (inits) memcpy(s.h_init, inits + i, n * 4);
     HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
@@ -1124,9 +1236,11 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     const int pflags = flags | AutoSplit(host_base, offsets + i, lengths + i, n) |
                        AutoLongHost(lengths + i, n);
     HostIndex hi;
-    rc = LaunchSpans(ctx, dev_base, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
-                     pflags, st, AutoLong::kNo, lane.FaultWord(),
-                     SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, st, &hi));
+    const HostIndex* hidx = SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, st, &hi);
+    // the kernel waits for the piece's copy (its descriptors went ahead)
+    if (dma) HCRC_CHECK(hipStreamWaitEvent(st, s.copied, 0));
+    rc = LaunchSpans(ctx, kbase, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
+                     pflags, st, AutoLong::kNo, lane.FaultWord(), hidx);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
@@ -1324,6 +1438,11 @@ __attribute__((visibility("default"))) void hcrc_test_clear_packed_meta() {
 __attribute__((visibility("default"))) void hcrc_test_packed_meta(uint32_t* out, int n) {
   for (int i = 0; i < n && i < static_cast<int>(lk::kPsMetaWords); ++i) out[i] = g_test_ps_meta[i];
 }
+// pinned-batch pieces since the last call: out[0] copy engine, out[1] zero-copy
+__attribute__((visibility("default"))) void hcrc_test_pinned_pieces(uint64_t* out) {
+  out[0] = g_test_dma_pieces.exchange(0);
+  out[1] = g_test_zc_pieces.exchange(0);
+}
 #endif
 
 int hcrc_device_count(int* count) {
@@ -1430,8 +1549,10 @@ hcrc_ctx::~hcrc_ctx() {
   DeviceGuard dg(device);
   for (auto& lane : lanes) {
     if (lane->stream) (void)hipStreamSynchronize(lane->stream);
+    if (lane->copy) (void)hipStreamSynchronize(lane->copy);
     for (Slot& s : lane->slots) s.Free();
     if (lane->stream) (void)hipStreamDestroy(lane->stream);
+    if (lane->copy) (void)hipStreamDestroy(lane->copy);
   }
   if (stream) (void)hipStreamSynchronize(stream);
   if (d_image) (void)hipFree(d_image);
