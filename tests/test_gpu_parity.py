@@ -1158,6 +1158,40 @@ print('BAD', bad)
 """
 
 
+def test_pinned_batches_see_fresh_bytes(engine, oracle):
+    """A pinned buffer reused call after call (TableBuilder's pooled write
+    buffers): every call sees the bytes and descriptors of its own moment --
+    the small zero-copy pieces read their descriptors and write their
+    results in the slot's pinned memory, the copy-engine pieces and the
+    zero-copy kernels read the caller's pinned bytes.  40 calls, the buffer
+    and the spans rewritten before each, against the oracle."""
+    import ctypes
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(77)
+    n = 24 << 20
+    p = ctypes.c_void_p()
+    _lib.check(lib.hcrc_host_alloc(n, ctypes.byref(p)), "host_alloc")
+    try:
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p.value))
+        for it in range(40):
+            big = it % 8 == 7  # every 8th call: a 20 MiB batch (copy engine)
+            k = 9000 if big else int(rng.integers(1, 3000))
+            lens = rng.integers(0, 4200, k).astype(np.uint32)
+            gaps = rng.integers(0, 64, k)
+            offs = (int(rng.integers(0, 4096)) +
+                    np.concatenate([[0], np.cumsum(lens.astype(np.int64) + gaps)[:-1]])).astype(np.uint64)
+            top = int(offs[-1]) + int(lens[-1])
+            buf[:top] = rng.integers(0, 256, top, dtype=np.uint8)
+            inits = (rng.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32)
+                     if it % 3 == 1 else None)
+            got = engine.batch(buf, offs, lens, inits)
+            np.testing.assert_array_equal(got, oracle.batch(np.asarray(buf), offs, lens, inits),
+                                          err_msg=f"call {it}")
+    finally:
+        lib.hcrc_host_free(p)
+
+
 @pytest.mark.parametrize("dma", ["1", "0"])
 def test_pinned_batches_copy_dense_pieces(dma):
     """Pinned / registered host batches: a dense, in-order piece of >= 8 MiB

@@ -134,20 +134,32 @@ constexpr uint32_t kPsMaxHostChunks = 16u * 1024u;
 constexpr size_t kPsHostWords = lk::kPsMetaWords + kPsMaxHostChunks + 1;
 
 // One piece of a host batch in flight: pinned host buffers and their device
-// mirrors.
+// mirrors.  A piece's descriptors -- offsets, lengths, inits and a
+// host-built HCRC_PACKED index (meta words + first[]) -- share one block
+// (Layout) and cross in one copy (SendDesc): each small copy costs
+// ~10 us of a one-SST call.
+constexpr size_t kDescBytes = kStageSpans * 16 + 3 * 256 + kPsHostWords * 4;
 struct Slot {
   uint8_t* h_data = nullptr;  // pinned
-  uint64_t* h_off = nullptr;  // pinned
+  uint8_t* h_desc = nullptr;  // pinned, kDescBytes
+  uint32_t* h_out = nullptr;  // pinned
+  uint8_t* d_data = nullptr;
+  uint8_t* d_desc = nullptr;
+  uint32_t* d_out = nullptr;
+  // device views of h_desc / h_out: a small zero-copy piece's kernel reads
+  // its descriptors and writes its results there (no copy either way)
+  uint8_t* hd_desc = nullptr;
+  uint32_t* hd_out = nullptr;
+  // the current piece's views of the descriptor blocks (Layout)
+  uint64_t* h_off = nullptr;
   uint32_t* h_len = nullptr;
   uint32_t* h_init = nullptr;
-  uint32_t* h_out = nullptr;
-  uint32_t* h_ps = nullptr;  // pinned: a host-built HCRC_PACKED index (meta words + first[])
-  uint8_t* d_data = nullptr;
+  uint32_t* h_ps = nullptr;
   uint64_t* d_off = nullptr;
   uint32_t* d_len = nullptr;
   uint32_t* d_init = nullptr;
-  uint32_t* d_out = nullptr;
   uint32_t* d_ps = nullptr;
+  size_t len_at = 0, init_at = 0, ps_at = 0;
   size_t cap_bytes = 0;
   hipEvent_t done = nullptr;
   // the copy engine's pieces of pinned batches (BatchZeroCopy): a device
@@ -160,17 +172,11 @@ struct Slot {
 
   void Free() {
     if (h_data) (void)hipHostFree(h_data);
-    if (h_off) (void)hipHostFree(h_off);
-    if (h_len) (void)hipHostFree(h_len);
-    if (h_init) (void)hipHostFree(h_init);
+    if (h_desc) (void)hipHostFree(h_desc);
     if (h_out) (void)hipHostFree(h_out);
-    if (h_ps) (void)hipHostFree(h_ps);
     if (d_data) (void)hipFree(d_data);
-    if (d_off) (void)hipFree(d_off);
-    if (d_len) (void)hipFree(d_len);
-    if (d_init) (void)hipFree(d_init);
+    if (d_desc) (void)hipFree(d_desc);
     if (d_out) (void)hipFree(d_out);
-    if (d_ps) (void)hipFree(d_ps);
     if (done) (void)hipEventDestroy(done);
     if (d_copy) (void)hipFree(d_copy);
     if (copied) (void)hipEventDestroy(copied);
@@ -186,24 +192,50 @@ struct Slot {
       if (e == hipSuccess) e = hipMalloc(p, n);
     };
     host(reinterpret_cast<void**>(&h_data), kStageBytes);
-    host(reinterpret_cast<void**>(&h_off), kStageSpans * 8);
-    host(reinterpret_cast<void**>(&h_len), kStageSpans * 4);
-    host(reinterpret_cast<void**>(&h_init), kStageSpans * 4);
+    host(reinterpret_cast<void**>(&h_desc), kDescBytes);
     host(reinterpret_cast<void**>(&h_out), kStageSpans * 4);
-    host(reinterpret_cast<void**>(&h_ps), kPsHostWords * 4);
     dev(reinterpret_cast<void**>(&d_data), kStageBytes);
-    dev(reinterpret_cast<void**>(&d_off), kStageSpans * 8);
-    dev(reinterpret_cast<void**>(&d_len), kStageSpans * 4);
-    dev(reinterpret_cast<void**>(&d_init), kStageSpans * 4);
+    dev(reinterpret_cast<void**>(&d_desc), kDescBytes);
     dev(reinterpret_cast<void**>(&d_out), kStageSpans * 4);
-    dev(reinterpret_cast<void**>(&d_ps), kPsHostWords * 4);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&hd_desc), h_desc, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&hd_out), h_out, 0);
     if (e != hipSuccess) {
       Free();
       return e == hipErrorOutOfMemory ? HCRC_ERR_NO_MEMORY : HCRC_ERR_HIP;
     }
     cap_bytes = kStageBytes;
     return HCRC_OK;
+  }
+  // The descriptor views for a piece of n (<= kStageSpans) spans: offsets,
+  // lengths, inits, the index, each 256-byte aligned.
+  void Layout(size_t n) {
+    auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
+    len_at = up(n * 8);
+    init_at = len_at + up(n * 4);
+    ps_at = init_at + up(n * 4);
+    h_off = reinterpret_cast<uint64_t*>(h_desc);
+    h_len = reinterpret_cast<uint32_t*>(h_desc + len_at);
+    h_init = reinterpret_cast<uint32_t*>(h_desc + init_at);
+    h_ps = reinterpret_cast<uint32_t*>(h_desc + ps_at);
+    d_off = reinterpret_cast<uint64_t*>(d_desc);
+    d_len = reinterpret_cast<uint32_t*>(d_desc + len_at);
+    d_init = reinterpret_cast<uint32_t*>(d_desc + init_at);
+    d_ps = reinterpret_cast<uint32_t*>(d_desc + ps_at);
+  }
+  // The same views with the device side on h_desc itself (a small
+  // zero-copy piece: the kernel reads the descriptors over PCIe).
+  void DirectLayout(size_t n) {
+    Layout(n);
+    d_off = reinterpret_cast<uint64_t*>(hd_desc);
+    d_len = reinterpret_cast<uint32_t*>(hd_desc + len_at);
+    d_init = reinterpret_cast<uint32_t*>(hd_desc + init_at);
+    d_ps = reinterpret_cast<uint32_t*>(hd_desc + ps_at);
+  }
+  // One copy of the piece's descriptors (+ inits, + ps_words of index).
+  hipError_t SendDesc(size_t n, bool inits, size_t ps_words, hipStream_t st) {
+    const size_t bytes = ps_words ? ps_at + ps_words * 4 : (inits ? init_at : len_at) + n * 4;
+    return hipMemcpyAsync(d_desc, h_desc, bytes, hipMemcpyHostToDevice, st);
   }
   // A data buffer of at least `bytes` (one span larger than the slot): the
   // new buffers are allocated before the old ones are released, so a
@@ -949,11 +981,12 @@ size_t HostPackedMinSpans() {
   return v;
 }
 
-// The piece's index into the slot (host copy, then H2D on st) when the piece
-// may take the packed kernel: no size-class / long-span flag, enough spans,
-// and the promise holds.  Returns the index to launch with, or nullptr.
+// The piece's index into the slot's descriptor block (it crosses with the
+// descriptors, Slot::SendDesc) when the piece may take the packed kernel: no
+// size-class / long-span flag, enough spans, and the promise holds.  Returns
+// the index to launch with, or nullptr.
 const HostIndex* SlotHostIndex(hcrc_ctx* ctx, Slot& s, const uint64_t* h_off, const uint32_t* h_len,
-                               size_t n, int flags, hipStream_t st, HostIndex* keep) {
+                               size_t n, int flags, HostIndex* keep) {
   if (flags & (HCRC_SPLIT_SMALL | HCRC_SPLIT_LONG | HCRC_BALANCE)) return nullptr;
   if (n < HostPackedMinSpans() || n <= kAutoLongSpans) return nullptr;
   const uint32_t C = static_cast<uint32_t>(PsChunksPerGroup() * LdsGrid(ctx, n));
@@ -964,9 +997,6 @@ const HostIndex* SlotHostIndex(hcrc_ctx* ctx, Slot& s, const uint64_t* h_off, co
   g_test_ps_meta[0] = s.h_ps[0] & 15u;
   g_test_ps_meta[7] = 0x484F5354u;  // ("HOST": the index was built on the host)
 #endif
-  if (hipMemcpyAsync(s.d_ps, s.h_ps, (lk::kPsMetaWords + C + 1) * 4, hipMemcpyHostToDevice, st) !=
-      hipSuccess)
-    return nullptr;
   keep->d_ps = s.d_ps;
   keep->C = C;
   return keep;
@@ -1138,6 +1168,9 @@ bool HostDma() {
 // piece of a batch after a copied one has no floor
 constexpr size_t kDmaBytes = size_t(128) << 20;
 constexpr size_t kDmaMinBytes = size_t(8) << 20;
+// zero-copy pieces of at most this many spans skip the descriptor and result
+// copies (Slot::DirectLayout)
+constexpr size_t kDirectSpans = 4096;
 
 // A dense piece of a pinned batch for the copy engine: spans [i, j) in
 // address order inside ONE pinned range whose covering bytes fit cap bytes
@@ -1207,6 +1240,12 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     ++(dma ? g_test_dma_pieces : g_test_zc_pieces);
 #endif
     const uint8_t* kbase = dev_base;
+    // a small zero-copy piece reads its descriptors and writes its results
+    // in pinned memory: its data crosses PCIe anyway, and a copy each way
+    // is ~10 us of a one-SST call
+    const bool direct = !dma && n <= kDirectSpans;
+    if (direct) s.DirectLayout(n);
+    else s.Layout(n);
     if (dma) {
       // the covering range at its address mod 256 in the slot
       const uintptr_t at = ca & 255u;
@@ -1230,19 +1269,19 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     }
     memcpy(s.h_len, lengths + i, n * 4);
     if (inits) memcpy(s.h_init, inits + i, n * 4);
-    HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
-    HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
-    if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
     const int pflags = flags | AutoSplit(host_base, offsets + i, lengths + i, n) |
                        AutoLongHost(lengths + i, n);
     HostIndex hi;
-    const HostIndex* hidx = SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, st, &hi);
+    const HostIndex* hidx = SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, &hi);
+    if (!direct)
+      HCRC_CHECK(s.SendDesc(n, inits != nullptr, hidx ? lk::kPsMetaWords + hidx->C + 1 : 0, st));
     // the kernel waits for the piece's copy (its descriptors went ahead)
     if (dma) HCRC_CHECK(hipStreamWaitEvent(st, s.copied, 0));
-    rc = LaunchSpans(ctx, kbase, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
-                     pflags, st, AutoLong::kNo, lane.FaultWord(), hidx);
+    rc = LaunchSpans(ctx, kbase, s.d_off, s.d_len, inits ? s.d_init : nullptr,
+                     direct ? s.hd_out : s.d_out, n, pflags, st, AutoLong::kNo, lane.FaultWord(),
+                     hidx);
     if (rc) return rc;
-    HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
+    if (!direct) HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));
     s.user_out = out + i;
     s.n_out = n;
@@ -1283,20 +1322,19 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     rc = s.Grow(bytes);
     if (rc) return rc;
     size_t used = 0;
-    PackSpans(s, base, offsets, lengths, inits, i, j, &used);
     const size_t n = j - i;
+    s.Layout(n);
+    PackSpans(s, base, offsets, lengths, inits, i, j, &used);
     HCRC_CHECK(hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, st));
-    HCRC_CHECK(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
-    HCRC_CHECK(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
-    if (inits) HCRC_CHECK(hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice, st));
     // (the staged layout is the slot's own: spans in order, 16-byte-aligned
     // cursor, gaps < 32 bytes -- packed whatever the caller's layout was)
     const int pflags = flags | AutoSplit(base, offsets + i, lengths + i, n) |
                        AutoLongHost(lengths + i, n);
     HostIndex hi;
+    const HostIndex* hidx = SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, &hi);
+    HCRC_CHECK(s.SendDesc(n, inits != nullptr, hidx ? lk::kPsMetaWords + hidx->C + 1 : 0, st));
     rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
-                     pflags, st, AutoLong::kNo, lane.FaultWord(),
-                     SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, st, &hi));
+                     pflags, st, AutoLong::kNo, lane.FaultWord(), hidx);
     if (rc) return rc;
     HCRC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost, st));
     HCRC_CHECK(hipEventRecord(s.done, st));

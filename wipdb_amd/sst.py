@@ -196,7 +196,8 @@ def merge_tables(images: Sequence[bytes], key_format: int = KEYS_INTERNAL, verif
 class PinnedImages:
     """Table images copied into one pinned host allocation (hcrc_host_alloc),
     the way a store would keep SST pages it checksums often: hcrc_batch
-    reads spans there zero-copy over PCIe instead of staging them."""
+    needs no staging copy there (dense pieces of >= 8 MiB go through the
+    copy engine, the rest is read zero-copy over PCIe)."""
 
     def __init__(self, images: Sequence[bytes]):
         from wipdb_amd import _lib as hl
