@@ -451,6 +451,15 @@ int main(int argc, char** argv) {
     RunSpans("table blocks", buf, Packed(l, 0, 4), l, nullptr, true, 3);
     g_want_pipe = 0;
   }
+  if (Want(argc, argv, "front pieces")) {
+    // pieces of every size 1..15 chunks (spans 4097..4336 B: both piece
+    // rings of run_ea, 8- and 16-chunk windows, interleaved), with inits
+    auto l = lens_of(3000, 4097, 4336);
+    auto in = inits_of(l.size());
+    g_want_pipe = 1;
+    RunSpans("front pieces 1..15 chunks", buf, Packed(l, 3, 4), l, &in, false, 3);
+    g_want_pipe = 0;
+  }
   if (Want(argc, argv, "near 4 KiB")) {
     auto l = lens_of(2000, 3960, 4240);
     auto in = inits_of(l.size());
