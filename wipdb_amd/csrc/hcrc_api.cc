@@ -467,6 +467,7 @@ class LaneLease {
     return HCRC_OK;
   }
   Lane* operator->() const { return lane_; }
+  Lane* get() const { return lane_; }
 
  private:
   hcrc_ctx* ctx_;
@@ -1205,6 +1206,30 @@ size_t DensePiece(const uint8_t* host_base, const uint64_t* offsets, const uint3
   return j;
 }
 
+// The lane's copy stream and the slot's copy buffer and event, made on first
+// use; false when the device cannot give them (nothing half-made is kept).
+bool CopyBuffers(Lane* lane, Slot& s) {
+  if (!lane->copy && hipStreamCreateWithFlags(&lane->copy, hipStreamNonBlocking) != hipSuccess) {
+    lane->copy = nullptr;
+    (void)hipGetLastError();
+    return false;
+  }
+  if (s.d_copy) return true;
+  if (hipMalloc(reinterpret_cast<void**>(&s.d_copy), kDmaBytes) != hipSuccess) {
+    s.d_copy = nullptr;
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) != hipSuccess) {
+    (void)hipFree(s.d_copy);
+    s.d_copy = nullptr;
+    s.copied = nullptr;
+    (void)hipGetLastError();
+    return false;
+  }
+  return true;
+}
+
 // Pinned batches: a dense piece (DensePiece) is copied into the slot's
 // d_copy by the copy engine -- the PCIe bytes are the covering range once,
 // at the copy engine's rate -- on the lane's copy stream, and the kernel
@@ -1230,9 +1255,11 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     // (the last piece after a copied one has no floor: its copy queues
     // behind that one's)
     uintptr_t ca = 0, cb = 0;
-    const size_t j =
+    size_t j =
         HostDma() ? DensePiece(host_base, offsets, lengths, i, count, kDmaBytes, copying, &ca, &cb)
                   : i;
+    // (no device memory or stream for the copy: the piece runs zero-copy)
+    if (j > i && !CopyBuffers(lane.get(), s)) j = i;
     const bool dma = j > i;
     copying = dma;
     const size_t n = dma ? j - i : std::min(count - i, kStageSpans);
@@ -1251,14 +1278,6 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
       const uintptr_t at = ca & 255u;
       const uintptr_t rebase = ca - at - reinterpret_cast<uintptr_t>(host_base);
       for (size_t q = 0; q < n; ++q) s.h_off[q] = offsets[i + q] - rebase;
-      if (!lane->copy) HCRC_CHECK(hipStreamCreateWithFlags(&lane->copy, hipStreamNonBlocking));
-      if (!s.d_copy) {
-        if (hipMalloc(reinterpret_cast<void**>(&s.d_copy), kDmaBytes) != hipSuccess) {
-          s.d_copy = nullptr;
-          return HCRC_ERR_NO_MEMORY;
-        }
-        HCRC_CHECK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
-      }
       // (the slot's previous piece is drained: its kernel is done with d_copy)
       HCRC_CHECK(hipMemcpyAsync(s.d_copy + at, reinterpret_cast<const void*>(ca), cb - ca,
                                 hipMemcpyHostToDevice, lane->copy));
