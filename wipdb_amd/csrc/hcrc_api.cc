@@ -1078,7 +1078,10 @@ class CopyPool {
     // a forked child inherits neither the helper threads nor consistent locks
     pthread_atfork(nullptr, nullptr, [] { g_forked_child.store(true); });
     const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = std::min(7u, hw > 1 ? hw - 1 : 0u);
+    unsigned nt = std::min(7u, hw > 1 ? hw - 1 : 0u);
+    // (WIPDB_COPY_THREADS: the helpers' count for A/Bs, at most 31)
+    if (const char* e = getenv("WIPDB_COPY_THREADS"))
+      if (*e) nt = std::min(31u, static_cast<unsigned>(atoi(e)));
     for (unsigned t = 0; t < nt; ++t) workers_.emplace_back([this, t] { Loop(t + 1); });
     for (auto& w : workers_) w.detach();
   }
