@@ -66,7 +66,7 @@ Also printed in the same JSON line:
                 Zipf-mixed SST-packed batch and its per-bucket GiB/s and p99
                 batch latency, WriteRawBlock-shaped table blocks and their
                 ReadBlock verify (device-resident), and config 5's 8Binsert
-                SST stream from pinned host memory (zero-copy, PCIe-inclusive)
+                SST stream from pinned host memory (copy engine, PCIe-inclusive)
                 against a measured PCIe H2D ceiling; every one sample-checked
                 against the reference's kv::crc32c (oracle/_ref).
 """

@@ -12,7 +12,8 @@ PCIe-inclusive host path) -- one JSON line each, for DESIGN.md.
              through hcrc_batch(HOST_PTRS): pinned staging + H2D + kernel +
              D2H, overlapped -- the PCIe-inclusive end-to-end rate.
   sstpin     config 5 from PINNED host memory (the table builder's write
-             buffers): zero-copy, as a fraction of the measured PCIe ceiling.
+             buffers): copy engine / zero-copy, as a fraction of the measured
+             PCIe ceiling.
   host4k     the headline 1 M x 4 KiB blocks from host memory (PCIe-inclusive).
 
 Every batch is checked against the library's host CPU path on a sample.
@@ -373,8 +374,8 @@ def run_sst_pinned(eng, rng, n_sst):
     """Config 5 through the product path the table layer takes: the SST
     stream in pinned host memory (hcrc_host_alloc -- TableBuilder's pooled
     write buffers are such memory), hcrc_batch(HOST_PTRS) finds every span
-    in it and runs zero-copy (the kernel reads the spans over PCIe), as a
-    fraction of the measured PCIe H2D ceiling."""
+    in it and needs no staging copy (dense pieces by the copy engine, the
+    rest zero-copy), as a fraction of the measured PCIe H2D ceiling."""
     import ctypes
     from wipdb_amd import _lib
     lib = _lib.load()
@@ -395,7 +396,7 @@ def run_sst_pinned(eng, rng, n_sst):
         ceiling = pcie_h2d_ceiling()
         rate = float(lens.sum()) / t / 2**30
         return {"config": "5 8Binsert SST stream in PINNED host memory (TableBuilder's write "
-                          "buffers), hcrc_batch HOST_PTRS -> zero-copy, PCIe-inclusive",
+                          "buffers), hcrc_batch HOST_PTRS -> copy engine / zero-copy, PCIe-inclusive",
                 "ssts": n_sst, "spans": int(offs.size), "bytes": int(lens.sum()),
                 "GiBps_end_to_end": round(rate, 2), "pcie_h2d_ceiling_GiBps": ceiling,
                 "fraction_of_pcie_ceiling": round(rate / ceiling, 3),
