@@ -1549,6 +1549,37 @@ def test_batch_multi_shards_on_one_device(oracle, golden_spans):
                                               g["inits"]), g["crc"])
 
 
+def test_batch_multi_pinned_dense_shards(oracle):
+    """hcrc_batch_multi_ex over a dense SST-like batch in pinned memory: each
+    shard (the device listed 1, 2 and 4 times: concurrent lanes of one
+    context) copies its >= 8 MiB pieces by the copy engine on its own lane's
+    copy stream; every shard OK, every CRC (inits, masked) equal to the
+    oracle's."""
+    import ctypes
+    from wipdb_amd import _lib, batch_multi
+    lib = _lib.load()
+    rng = np.random.default_rng(88)
+    lens = rng.integers(4097, 4226, 11000).astype(np.uint32)
+    offs = (5 + np.concatenate([[0], np.cumsum(lens.astype(np.int64) + 4)[:-1]])).astype(np.uint64)
+    n = int(offs[-1]) + int(lens[-1]) + 64
+    inits = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    p = ctypes.c_void_p()
+    _lib.check(lib.hcrc_host_alloc(n, ctypes.byref(p)), "host_alloc")
+    try:
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p.value))
+        buf[:] = rng.integers(0, 256, n, dtype=np.uint8)
+        want = oracle.batch(np.asarray(buf), offs, lens, inits)
+        wantm = oracle.batch(np.asarray(buf), offs, lens, inits, mask=True)
+        for devs in ([0], [0, 0], [0, 0, 0, 0]):
+            got, rcs = batch_multi(devs, buf, offs, lens, inits, shard_status=True)
+            assert rcs == [0] * len(devs)
+            np.testing.assert_array_equal(got, want, err_msg=str(devs))
+            got = batch_multi(devs, buf, offs, lens, inits, mask_output=True)
+            np.testing.assert_array_equal(got, wantm, err_msg=str(devs))
+    finally:
+        lib.hcrc_host_free(p)
+
+
 def test_batch_multi_failing_device_fails_its_shard_only(oracle):
     """A shard on a device that does not exist returns HCRC_ERR_NO_DEVICE for
     that shard alone; the other shard's results are still right."""
