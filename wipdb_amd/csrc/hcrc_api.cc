@@ -1492,6 +1492,26 @@ __attribute__((visibility("default"))) uint32_t hcrc_test_host_ps_index(const ui
                                                                         uint32_t* ps) {
   return HostPsIndex(off, len, n, C, ps);
 }
+// The copy engine's piece choice (DensePiece) over a host range entered as
+// pinned without pinning it (hcrc_test_fake_pinned_range; bytes 0 removes
+// it), for the CPU test of the piece rules: returns j, and [a, b) as
+// offsets from host_base.
+__attribute__((visibility("default"))) void hcrc_test_fake_pinned_range(void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  if (bytes) HostRanges()[reinterpret_cast<uintptr_t>(p)] = {bytes, static_cast<uint8_t*>(p)};
+  else HostRanges().erase(reinterpret_cast<uintptr_t>(p));
+}
+__attribute__((visibility("default"))) size_t hcrc_test_dense_piece(const uint8_t* host_base,
+                                                                   const uint64_t* offsets,
+                                                                   const uint32_t* lengths,
+                                                                   size_t i, size_t count, int tail,
+                                                                   uint64_t* ab) {
+  uintptr_t a = 0, b = 0;
+  const size_t j = DensePiece(host_base, offsets, lengths, i, count, kDmaBytes, tail != 0, &a, &b);
+  ab[0] = a - reinterpret_cast<uintptr_t>(host_base);
+  ab[1] = b - reinterpret_cast<uintptr_t>(host_base);
+  return j;
+}
 __attribute__((visibility("default"))) void hcrc_test_clear_packed_meta() {
   for (uint32_t k = 0; k < lk::kPsMetaWords; ++k) g_test_ps_meta[k] = 0xFFFFFFFFu;
 }
