@@ -1580,6 +1580,43 @@ def test_batch_multi_pinned_dense_shards(oracle):
         lib.hcrc_host_free(p)
 
 
+def test_config5_pinned_full_batch(engine, oracle):
+    """BASELINE config 5 at full size through the product path: 256 SSTs of
+    the 8Binsert shape (per SST 480-519 data blocks of 4097..4225 B, an index,
+    a filter and a metaindex block, 4-byte trailers, a 48-byte footer; ~550
+    MB) in hcrc_host_alloc memory, one hcrc_batch call (copy-engine pieces
+    of 128 MiB), EVERY CRC (masked, as WriteRawBlock stamps it) against the
+    oracle."""
+    import ctypes
+    from wipdb_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(0xC5)
+    offs, lens, cur = [], [], 0
+    for _ in range(256):
+        for _ in range(int(rng.integers(480, 520))):
+            n = int(rng.integers(4096, 4225)) + 1
+            offs.append(cur)
+            lens.append(n)
+            cur += n + 4
+        for n in (int(rng.integers(15000, 20000)), int(rng.integers(24000, 26000)),
+                  int(rng.integers(40, 100))):
+            offs.append(cur)
+            lens.append(n + 1)
+            cur += n + 5
+        cur += 48
+    offs = np.array(offs, np.uint64)
+    lens = np.array(lens, np.uint32)
+    p = ctypes.c_void_p()
+    _lib.check(lib.hcrc_host_alloc(cur, ctypes.byref(p)), "host_alloc")
+    try:
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * cur).from_address(p.value))
+        buf[:] = rng.integers(32, 127, cur, dtype=np.uint8)
+        got = engine.batch(buf, offs, lens, mask_output=True)
+        np.testing.assert_array_equal(got, oracle.batch(np.asarray(buf), offs, lens, mask=True))
+    finally:
+        lib.hcrc_host_free(p)
+
+
 def test_batch_multi_failing_device_fails_its_shard_only(oracle):
     """A shard on a device that does not exist returns HCRC_ERR_NO_DEVICE for
     that shard alone; the other shard's results are still right."""
