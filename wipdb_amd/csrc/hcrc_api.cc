@@ -1209,24 +1209,29 @@ size_t DensePiece(const uint8_t* host_base, const uint64_t* offsets, const uint3
   return j;
 }
 
-// The lane's copy stream and the slot's copy buffer and event, made on first
-// use; false when the device cannot give them (nothing half-made is kept).
-bool CopyBuffers(Lane* lane, Slot& s) {
+// The lane's copy stream and the slot's copy event, made on first use; false
+// when the device cannot give them.
+bool CopyStream(Lane* lane, Slot& s) {
   if (!lane->copy && hipStreamCreateWithFlags(&lane->copy, hipStreamNonBlocking) != hipSuccess) {
     lane->copy = nullptr;
     (void)hipGetLastError();
     return false;
   }
-  if (s.d_copy) return true;
-  if (hipMalloc(reinterpret_cast<void**>(&s.d_copy), kDmaBytes) != hipSuccess) {
-    s.d_copy = nullptr;
+  if (!s.copied && hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) != hipSuccess) {
+    s.copied = nullptr;
     (void)hipGetLastError();
     return false;
   }
-  if (hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) != hipSuccess) {
-    (void)hipFree(s.d_copy);
+  return true;
+}
+
+// The same and the slot's copy buffer, made on first use; false when the
+// device cannot give them (nothing half-made is kept).
+bool CopyBuffers(Lane* lane, Slot& s) {
+  if (!CopyStream(lane, s)) return false;
+  if (s.d_copy) return true;
+  if (hipMalloc(reinterpret_cast<void**>(&s.d_copy), kDmaBytes) != hipSuccess) {
     s.d_copy = nullptr;
-    s.copied = nullptr;
     (void)hipGetLastError();
     return false;
   }
@@ -1347,7 +1352,13 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     const size_t n = j - i;
     s.Layout(n);
     PackSpans(s, base, offsets, lengths, inits, i, j, &used);
-    HCRC_CHECK(hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, st));
+    // a big piece's bytes go on the lane's copy stream, so the next piece's
+    // copy runs under this piece's kernel and results (a small one stays on
+    // the lane's stream: no cross-stream wait in a one-SST call)
+    const bool ahead = used >= kDmaMinBytes && CopyStream(lane.get(), s);
+    HCRC_CHECK(hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice,
+                              ahead ? lane->copy : st));
+    if (ahead) HCRC_CHECK(hipEventRecord(s.copied, lane->copy));
     // (the staged layout is the slot's own: spans in order, 16-byte-aligned
     // cursor, gaps < 32 bytes -- packed whatever the caller's layout was)
     const int pflags = flags | AutoSplit(base, offsets + i, lengths + i, n) |
@@ -1355,6 +1366,7 @@ int BatchHost(hcrc_ctx* ctx, const uint8_t* base, const uint64_t* offsets, const
     HostIndex hi;
     const HostIndex* hidx = SlotHostIndex(ctx, s, s.h_off, s.h_len, n, pflags, &hi);
     HCRC_CHECK(s.SendDesc(n, inits != nullptr, hidx ? lk::kPsMetaWords + hidx->C + 1 : 0, st));
+    if (ahead) HCRC_CHECK(hipStreamWaitEvent(st, s.copied, 0));
     rc = LaunchSpans(ctx, s.d_data, s.d_off, s.d_len, inits ? s.d_init : nullptr, s.d_out, n,
                      pflags, st, AutoLong::kNo, lane.FaultWord(), hidx);
     if (rc) return rc;
