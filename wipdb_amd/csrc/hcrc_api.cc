@@ -1284,12 +1284,13 @@ int BatchZeroCopy(hcrc_ctx* ctx, LaneLease& lane, const uint8_t* dev_base,
     if (dma) {
       // the covering range at its address mod 256 in the slot
       const uintptr_t at = ca & 255u;
-      const uintptr_t rebase = ca - at - reinterpret_cast<uintptr_t>(host_base);
-      for (size_t q = 0; q < n; ++q) s.h_off[q] = offsets[i + q] - rebase;
-      // (the slot's previous piece is drained: its kernel is done with d_copy)
+      // (the slot's previous piece is drained: its kernel is done with d_copy;
+      // the copy goes out first, the descriptors are written under it)
       HCRC_CHECK(hipMemcpyAsync(s.d_copy + at, reinterpret_cast<const void*>(ca), cb - ca,
                                 hipMemcpyHostToDevice, lane->copy));
       HCRC_CHECK(hipEventRecord(s.copied, lane->copy));
+      const uintptr_t rebase = ca - at - reinterpret_cast<uintptr_t>(host_base);
+      for (size_t q = 0; q < n; ++q) s.h_off[q] = offsets[i + q] - rebase;
       kbase = s.d_copy;
     } else {
       memcpy(s.h_off, offsets + i, n * 8);
